@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node images/sec, ResNet-50 bf16 DDP training, synthetic ImageNet.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch resnet50] [--batch 256]
+                    [--impl native|torch] [--bucket-mb 25] [--wire-dtype fp32|bf16]
+
+For N > 1 it is launched one process per GPU by torchrun (RANK/LOCAL_RANK/
+WORLD_SIZE/MASTER_* from the env); if started without torchrun and --gpus > 1
+it re-launches itself through ``torch.distributed.run`` (before touching the GPU).
+
+A timed step is the full reference training step (``resnet/main.py:119-124``):
+zero_grad, forward (incl. NCHW fp32 image -> NHWC bf16), cross-entropy, backward
+with bucketed gradient all-reduce over RCCL, SGD(momentum 0.9, wd 1e-5) update.
+Per-GPU batch is fixed (256, the reference's per-process batch) so scaling is
+weak.  W warmup steps, then exactly K steps bracketed by barrier +
+synchronize; the reported time is the MAX over ranks.  ``--impl torch`` runs
+the stock PyTorch-ROCm path (torch DDP + MIOpen/hipBLASLt via autocast bf16,
+channels_last, foreach SGD) = the comparison baseline of BASELINE.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+# Stock PyTorch-ROCm DDP ResNet-50 bf16 (bench.py --impl torch) measured on MI355X, img/s
+# per N -- the baseline to beat (BASELINE.md "Measured stock baseline"); None = unmeasured.
+STOCK_BASELINE_IMG_S = {1: None, 2: None, 4: None, 8: None}
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--arch", default="resnet50")
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--num-classes", type=int, default=1000)
+    p.add_argument("--impl", default="native", choices=["native", "torch"])
+    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--json-out", default=None)
+    return p.parse_args(argv)
+
+
+def _relaunch_with_torchrun(args_argv, n) -> int:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29511"),
+           os.path.abspath(__file__)] + args_argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _relaunch_with_torchrun(argv, args.gpus)
+
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.optim import SGD
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel, init_distributed
+
+    env = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+    world = env.world_size
+    dev = torch.device(f"cuda:{env.local_rank}" if torch.cuda.is_available() else "cpu")
+    torch.manual_seed(0)
+
+    if args.impl == "native":
+        model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
+        model.set_impl("native")
+        ddp = DistributedDataParallel(model, device_ids=[env.local_rank], output_device=env.local_rank,
+                                      bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
+        opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+        criterion = ops.CrossEntropyLoss()
+        autocast = None
+    else:
+        model = build_model(args.arch, num_classes=args.num_classes, impl="torch").to(dev)
+        model = model.to(memory_format=torch.channels_last)
+        if world > 1:
+            ddp = nn.parallel.DistributedDataParallel(model, device_ids=[env.local_rank],
+                                                      output_device=env.local_rank,
+                                                      bucket_cap_mb=args.bucket_mb)
+        else:
+            ddp = model
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+        criterion = nn.CrossEntropyLoss()
+        autocast = torch.bfloat16
+
+    g = torch.Generator(device="cpu").manual_seed(1234 + env.rank)
+    images = torch.randn((args.batch, 3, args.image_size, args.image_size), generator=g).to(dev)
+    labels = torch.randint(0, args.num_classes, (args.batch,), generator=g).to(dev)
+    if args.impl == "torch":
+        images = images.contiguous(memory_format=torch.channels_last)
+
+    def step():
+        opt.zero_grad()
+        if autocast is not None:
+            with torch.autocast("cuda", dtype=autocast):
+                out = ddp(images)
+                loss = criterion(out, labels)
+        else:
+            out = ddp(images)
+            loss = criterion(out, labels)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        loss = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    if env.rank == 0:
+        img_s = world * args.batch * args.steps / elapsed
+        base = STOCK_BASELINE_IMG_S.get(world)
+        res = {
+            "metric": "images/sec (whole node) ResNet-50 bf16 at 1/2/4/8 MI355X"
+            if args.arch == "resnet50" else f"images/sec (whole node) {args.arch} bf16",
+            "value": round(img_s, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(img_s / base, 4) if base else None),
+            "dtype": "bf16",
+            "data": "synthetic (ImageNet-shaped 3x224x224 fp32 images, random labels, random-init weights)",
+            "config": {"model": args.arch, "global_batch": args.batch * world,
+                       "seq_len": None, "image_size": args.image_size,
+                       "parallelism": f"dp{world}", "impl": args.impl,
+                       "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype,
+                       "final_loss": round(final_loss, 4)},
+        }
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

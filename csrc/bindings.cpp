@@ -1,0 +1,379 @@
+// Python bindings of the native extension `pytorch_distributed_tutorials_amd._C`.
+//
+// Adapts torch tensors to the raw-pointer launchers of csrc/kernels (which are
+// compiled without any PyTorch headers), allocates outputs/workspaces through
+// the PyTorch caching allocator and launches on the current HIP stream, so the
+// ops compose with autograd, streams and graph capture.  Also exposes the RCCL
+// communicator and the gradient reducer.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <optional>
+
+#include "comm/rccl_comm.h"
+#include "ddp/reducer.h"
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.get_device()).stream();
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_bf16_nhwc(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.dim() == 4, name, " must be 4-D NHWC");
+  TORCH_CHECK(t.size(3) % 8 == 0, name, " channels must be a multiple of 8");
+  TORCH_CHECK(t.numel() < (int64_t(1) << 30), name, " too large for 32-bit buffer addressing");
+}
+
+uint16_t* bf(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* cbf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+
+// ------------------------------------------------------------------ layout
+Tensor image_to_nhwc(const Tensor& x) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 4, "image must be fp32 NCHW");
+  c10::hip::HIPGuard g(x.get_device());
+  int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  int Cp = ((C + 7) / 8) * 8;
+  auto y = at::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  pdt::launch_image_to_nhwc(x.data_ptr<float>(), bf(y), N, C, H, W, Cp, cur_stream(x));
+  return y;
+}
+
+Tensor pack_weight(const Tensor& w, int64_t cpad) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kFloat, "weight must be fp32 4-D");
+  c10::hip::HIPGuard g(w.get_device());
+  int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  int Cp = std::max<int>((int)cpad, C);
+  auto out = at::empty({K, R, S, Cp}, w.options().dtype(at::kBFloat16));
+  int64_t st[4] = {w.stride(0), w.stride(1), w.stride(2), w.stride(3)};
+  pdt::launch_pack_weight(w.data_ptr<float>(), st, bf(out), K, C, R, S, Cp, cur_stream(w));
+  return out;
+}
+
+Tensor pack_weight_t(const Tensor& w) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kFloat, "weight must be fp32 4-D");
+  c10::hip::HIPGuard g(w.get_device());
+  int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  auto out = at::empty({C, R, S, K}, w.options().dtype(at::kBFloat16));
+  int64_t st[4] = {w.stride(0), w.stride(1), w.stride(2), w.stride(3)};
+  pdt::launch_pack_weight_t(w.data_ptr<float>(), st, bf(out), K, C, R, S, cur_stream(w));
+  return out;
+}
+
+// -------------------------------------------------------------------- conv
+pdt::ConvShape shape_of(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+  pdt::ConvShape s;
+  s.N = N; s.H = H; s.W = W; s.C = C; s.K = K; s.R = R; s.S = S;
+  s.stride = stride; s.pad = pad;
+  s.Ho = (H + 2 * pad - R) / stride + 1;
+  s.Wo = (W + 2 * pad - S) / stride + 1;
+  return s;
+}
+
+// returns (y, part); part is empty when stats == false
+std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& wk, int64_t stride, int64_t pad,
+                                    bool stats) {
+  check_bf16_nhwc(x, "x");
+  check_cuda(wk, "wk");
+  TORCH_CHECK(wk.dim() == 4 && wk.size(3) == x.size(3), "packed weight must be [K,R,S,Cx]");
+  c10::hip::HIPGuard g(x.get_device());
+  auto s = shape_of(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2),
+                    stride, pad);
+  TORCH_CHECK(s.K % 8 == 0, "output channels must be a multiple of 8");
+  auto y = at::empty({s.N, s.Ho, s.Wo, s.K}, x.options());
+  Tensor part;
+  float* pp = nullptr;
+  int M = s.N * s.Ho * s.Wo;
+  if (stats) {
+    int grows = pdt::conv_fwd_group_rows(M, s.K);
+    int ng = (M + grows - 1) / grows;
+    part = at::empty({ng, 2, s.K}, x.options().dtype(at::kFloat));
+    pp = part.data_ptr<float>();
+  }
+  pdt::launch_conv_fwd(cbf(x), cbf(wk), bf(y), pp, s, cur_stream(x));
+  return {y, part};
+}
+
+Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, int64_t stride,
+                  int64_t pad) {
+  check_bf16_nhwc(dy, "dy");
+  TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
+  TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
+  c10::hip::HIPGuard g(dy.get_device());
+  auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
+  TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
+  Tensor wt = pack_weight_t(w);
+  auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
+  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), s, cur_stream(dy));
+  return dx;
+}
+
+// dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
+Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
+                  int64_t pad) {
+  check_bf16_nhwc(dy, "dy");
+  check_bf16_nhwc(x, "x");
+  TORCH_CHECK(ws.size() == 4, "weight shape must be [K,C,R,S]");
+  c10::hip::HIPGuard g(x.get_device());
+  int K = ws[0], C = ws[1], R = ws[2], S = ws[3];
+  int Cx = x.size(3);
+  auto s = shape_of(x.size(0), x.size(1), x.size(2), Cx, K, R, S, stride, pad);
+  TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && K == dy.size(3), "wgrad: dy shape mismatch");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dwp = at::empty({K, R, S, Cx}, fopt);
+  size_t wsn = pdt::conv_wgrad_ws_floats(s);
+  Tensor wsb = wsn ? at::empty({(int64_t)wsn}, fopt) : Tensor();
+  pdt::launch_conv_wgrad(cbf(dy), cbf(x), dwp.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
+                         s, cur_stream(x));
+  Tensor krsc = Cx == C ? dwp : dwp.narrow(3, 0, C).contiguous();
+  return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
+}
+
+// ---------------------------------------------------------------------- BN
+Tensor bn_finalize(const Tensor& part, int64_t count, const Tensor& rm, const Tensor& rv,
+                   const Tensor& gamma, const Tensor& beta, double momentum, double eps) {
+  check_cuda(part, "part");
+  c10::hip::HIPGuard g(part.get_device());
+  int ng = part.size(0), K = part.size(2);
+  int grows = pdt::conv_fwd_group_rows((int)count, K);
+  TORCH_CHECK((count + grows - 1) / grows == ng, "bn_finalize: partial layout mismatch");
+  int P = pdt::bn_finalize_partitions(ng);
+  auto out = at::empty({4 * K + 3 * K * P}, part.options());
+  TORCH_CHECK(gamma.scalar_type() == at::kFloat && rm.scalar_type() == at::kFloat, "BN params must be fp32");
+  pdt::launch_bn_finalize(part.data_ptr<float>(), ng, grows, (int)count, K,
+                          rm.defined() ? rm.data_ptr<float>() : nullptr,
+                          rv.defined() ? rv.data_ptr<float>() : nullptr, gamma.data_ptr<float>(),
+                          beta.data_ptr<float>(), (float)momentum, (float)eps,
+                          out.data_ptr<float>(), cur_stream(part));
+  return out.narrow(0, 0, 4 * K).view({4, K});
+}
+
+Tensor bn_eval_params(const Tensor& rm, const Tensor& rv, const Tensor& gamma, const Tensor& beta,
+                      double eps) {
+  check_cuda(rm, "running_mean");
+  c10::hip::HIPGuard g(rm.get_device());
+  int K = rm.numel();
+  auto out = at::empty({4, K}, rm.options().dtype(at::kFloat));
+  pdt::launch_bn_eval_params(rm.data_ptr<float>(), rv.data_ptr<float>(), gamma.data_ptr<float>(),
+                             beta.data_ptr<float>(), (float)eps, K, out.data_ptr<float>(),
+                             cur_stream(rm));
+  return out;
+}
+
+Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
+                  const std::optional<Tensor>& res, bool relu) {
+  check_bf16_nhwc(y, "y");
+  c10::hip::HIPGuard g(y.get_device());
+  int K = y.size(3);
+  int64_t M = y.numel() / K;
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_nhwc(*res, "residual");
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
+    rp = cbf(*res);
+  }
+  auto z = at::empty_like(y);
+  pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z), M,
+                         K, cur_stream(y));
+  return z;
+}
+
+Tensor bn_act_bwd_reduce(const Tensor& dz, const Tensor& z, const Tensor& y, const Tensor& mean,
+                         bool relu) {
+  check_bf16_nhwc(dz, "dz");
+  check_bf16_nhwc(y, "y");
+  c10::hip::HIPGuard g(dz.get_device());
+  int K = y.size(3);
+  TORCH_CHECK(256 % (K / 8) == 0, "bn backward: channels must divide 2048 and be a power of two");
+  int64_t M = y.numel() / K;
+  auto fopt = y.options().dtype(at::kFloat);
+  auto ws = at::empty({(int64_t)pdt::bn_bwd_ws_floats(M, K)}, fopt);
+  auto sums = at::empty({2, K}, fopt);
+  pdt::launch_bn_act_bwd_reduce(cbf(dz), cbf(z), cbf(y), mean.data_ptr<float>(), relu, M, K,
+                                ws.data_ptr<float>(), sums.data_ptr<float>(), cur_stream(y));
+  return sums;
+}
+
+std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, const Tensor& y,
+                                            const Tensor& mean, const Tensor& invstd,
+                                            const Tensor& gamma, const Tensor& sums, bool relu,
+                                            bool training, bool want_dres) {
+  check_bf16_nhwc(dz, "dz");
+  c10::hip::HIPGuard g(dz.get_device());
+  int K = y.size(3);
+  int64_t M = y.numel() / K;
+  auto dy = at::empty_like(dz);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(dz);
+  pdt::launch_bn_act_bwd_apply(cbf(dz), cbf(z), cbf(y), mean.data_ptr<float>(),
+                               invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                               sums.data_ptr<float>(), relu, training, M, K, bf(dy),
+                               want_dres ? bf(dres) : nullptr, cur_stream(dz));
+  return {dy, dres};
+}
+
+// -------------------------------------------------------------------- pool
+std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x) {
+  check_bf16_nhwc(x, "x");
+  c10::hip::HIPGuard g(x.get_device());
+  int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  auto idx = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  pdt::launch_maxpool_fwd(cbf(x), bf(y), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, cur_stream(x));
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, int64_t H, int64_t W) {
+  check_bf16_nhwc(dy, "dy");
+  c10::hip::HIPGuard g(dy.get_device());
+  int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  pdt::launch_maxpool_bwd(cbf(dy), idx.data_ptr<uint8_t>(), bf(dx), N, H, W, C, Ho, Wo, cur_stream(dy));
+  return dx;
+}
+
+Tensor avgpool_fwd(const Tensor& x) {
+  check_bf16_nhwc(x, "x");
+  c10::hip::HIPGuard g(x.get_device());
+  int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = at::empty({N, C}, x.options().dtype(at::kFloat));
+  pdt::launch_avgpool_fwd(cbf(x), y.data_ptr<float>(), N, HW, C, cur_stream(x));
+  return y;
+}
+
+Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
+  check_cuda(dy, "dy");
+  c10::hip::HIPGuard g(dy.get_device());
+  int N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options().dtype(at::kBFloat16));
+  pdt::launch_avgpool_bwd(dy.data_ptr<float>(), bf(dx), N, (int)(H * W), C, cur_stream(dy));
+  return dx;
+}
+
+// -------------------------------------------------------------------- head
+std::tuple<Tensor, Tensor> softmax_xent(const Tensor& logits_in, const Tensor& labels) {
+  check_cuda(logits_in, "logits");
+  c10::hip::HIPGuard g(logits_in.get_device());
+  Tensor logits = logits_in.scalar_type() == at::kFloat ? logits_in : logits_in.to(at::kFloat);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  int N = logits.size(0), V = logits.size(1);
+  auto loss = at::empty({}, logits.options());
+  auto dl = at::empty_like(logits);
+  auto ws = at::empty({N}, logits.options());
+  pdt::launch_softmax_xent(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                           dl.data_ptr<float>(), ws.data_ptr<float>(), N, V, cur_stream(logits));
+  return {loss, dl};
+}
+
+Tensor top1_correct(const Tensor& logits_in, const Tensor& labels) {
+  check_cuda(logits_in, "logits");
+  c10::hip::HIPGuard g(logits_in.get_device());
+  Tensor logits = logits_in.scalar_type() == at::kFloat ? logits_in : logits_in.to(at::kFloat);
+  int N = logits.size(0), V = logits.size(1);
+  auto cnt = at::empty({}, labels.options().dtype(at::kLong));
+  pdt::launch_top1(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), cnt.data_ptr<int64_t>(), N, V,
+                   cur_stream(logits));
+  return cnt;
+}
+
+// --------------------------------------------------------------------- sgd
+void sgd_step(Tensor p, const Tensor& g, Tensor buf, double lr, double momentum, double dampening,
+              double wd, bool nesterov, bool first, double grad_scale) {
+  check_cuda(p, "param");
+  check_cuda(g, "grad");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 flat buffers only");
+  TORCH_CHECK(p.numel() == g.numel(), "param/grad size mismatch");
+  bool mom = momentum != 0.0;
+  if (mom) {
+    check_cuda(buf, "momentum_buffer");
+    TORCH_CHECK(buf.numel() == p.numel(), "momentum buffer size mismatch");
+  }
+  auto aligned = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  TORCH_CHECK(aligned(p.data_ptr()) && aligned(g.data_ptr()) && (!mom || aligned(buf.data_ptr())),
+              "sgd_step: flat buffers must be 16-byte aligned");
+  c10::hip::HIPGuard gd(p.get_device());
+  pdt::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), mom ? buf.data_ptr<float>() : nullptr,
+                  p.numel(), (float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first,
+                  (float)grad_scale, cur_stream(p));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X (gfx950) native kernels, RCCL communicator and DDP reducer";
+  m.def("image_to_nhwc", &image_to_nhwc);
+  m.def("pack_weight", &pack_weight, py::arg("w"), py::arg("cpad") = 0);
+  m.def("pack_weight_t", &pack_weight_t);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
+        py::arg("stats"));
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_params", &bn_eval_params);
+  m.def("bn_act_fwd", &bn_act_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"),
+        py::arg("residual"), py::arg("relu"));
+  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce);
+  m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("top1_correct", &top1_correct);
+  m.def("sgd_step", &sgd_step);
+  m.def("conv_fwd_group_rows", &pdt::conv_fwd_group_rows);
+
+  py::class_<pdt::RcclComm, std::shared_ptr<pdt::RcclComm>>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(pdt::RcclComm::unique_id()); })
+      .def(py::init([](const std::string& uid, int rank, int world, int device) {
+             py::gil_scoped_release nogil;  // ncclCommInitRank blocks until all ranks join
+             return std::make_shared<pdt::RcclComm>(uid, rank, world, device);
+           }))
+      .def_property_readonly("rank", &pdt::RcclComm::rank)
+      .def_property_readonly("world", &pdt::RcclComm::world)
+      .def_property_readonly("device", &pdt::RcclComm::device)
+      .def_property_readonly("stream_ptr",
+                             [](const pdt::RcclComm& c) { return reinterpret_cast<uintptr_t>(c.stream()); })
+      .def("all_reduce", &pdt::RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum",
+           py::arg("wait_current") = true)
+      .def("broadcast", &pdt::RcclComm::broadcast, py::arg("t"), py::arg("root") = 0,
+           py::arg("wait_current") = true)
+      .def("reduce_scatter", &pdt::RcclComm::reduce_scatter, py::arg("inp"), py::arg("out"),
+           py::arg("op") = "sum", py::arg("wait_current") = true)
+      .def("all_gather", &pdt::RcclComm::all_gather, py::arg("inp"), py::arg("out"),
+           py::arg("wait_current") = true)
+      .def("comm_wait_current", &pdt::RcclComm::comm_wait_current)
+      .def("current_wait_comm", &pdt::RcclComm::current_wait_comm)
+      .def("synchronize", &pdt::RcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &pdt::RcclComm::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &pdt::RcclComm::abort);
+
+  py::class_<pdt::Reducer>(m, "Reducer")
+      .def(py::init<std::vector<Tensor>, std::vector<Tensor>, std::vector<int64_t>, std::vector<Tensor>,
+                    std::shared_ptr<pdt::RcclComm>, py::object, py::object, bool, std::string>(),
+           py::arg("params"), py::arg("grad_views"), py::arg("bucket_of_param"),
+           py::arg("bucket_flats"), py::arg("comm"), py::arg("py_launch"), py::arg("py_finalize"),
+           py::arg("average") = true, py::arg("wire_dtype") = "fp32")
+      .def("prepare_for_backward", &pdt::Reducer::prepare_for_backward,
+           py::call_guard<py::gil_scoped_release>())
+      .def("set_enabled", &pdt::Reducer::set_enabled)
+      .def_property_readonly("enabled", &pdt::Reducer::enabled)
+      .def_property_readonly("num_buckets", &pdt::Reducer::num_buckets)
+      .def_property_readonly("iterations", &pdt::Reducer::iterations)
+      .def("last_launch_order", &pdt::Reducer::last_launch_order);
+}

@@ -1,0 +1,195 @@
+#include "reducer.h"
+
+#include <c10/hip/HIPGuard.h>
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/autograd/variable.h>
+
+#include <stdexcept>
+
+#include "../kernels/kernels.h"
+
+namespace py = pybind11;
+
+namespace pdt {
+
+struct ReducerState {
+  std::vector<at::Tensor> params;
+  std::vector<at::Tensor> views;
+  std::vector<int64_t> bucket_of;
+  std::vector<at::Tensor> flats;
+  std::vector<std::vector<int64_t>> members;  // params per bucket
+  std::shared_ptr<RcclComm> comm;
+  py::object py_launch, py_finalize;
+  bool average = true;
+  bool wire_bf16 = false;
+  std::vector<at::Tensor> wire;  // bf16 staging per bucket (lazy)
+
+  std::vector<std::shared_ptr<torch::autograd::Node>> accumulators;
+
+  std::mutex mu;
+  bool enabled = true;
+  bool expecting = false;
+  bool callback_queued = false;
+  std::vector<int64_t> pending;
+  std::vector<char> param_ready;
+  std::vector<char> bucket_ready;
+  int64_t next_launch = 0;
+  std::vector<int64_t> launch_order, last_order;
+  int64_t iters = 0;
+
+  void reset_counters() {
+    pending.assign(flats.size(), 0);
+    for (size_t b = 0; b < flats.size(); ++b) pending[b] = (int64_t)members[b].size();
+    param_ready.assign(params.size(), 0);
+    bucket_ready.assign(flats.size(), 0);
+    next_launch = 0;
+    launch_order.clear();
+  }
+
+  void launch_bucket(int64_t b) {
+    launch_order.push_back(b);
+    if (comm) {
+      const at::Tensor& f = flats[b];
+      c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
+      comm->comm_wait_current();
+      hipStream_t cs = comm->stream();
+      if (wire_bf16) {
+        if (!wire[b].defined())
+          wire[b] = at::empty({f.numel()}, f.options().dtype(at::kBFloat16));
+        launch_cast_f32_bf16(f.data_ptr<float>(), reinterpret_cast<uint16_t*>(wire[b].data_ptr()),
+                             f.numel(), cs);
+        comm->all_reduce_raw(wire[b].data_ptr(), (size_t)f.numel(), ncclBfloat16, ncclSum);
+        float scale = average ? 1.f / (float)comm->world() : 1.f;
+        launch_cast_bf16_f32(reinterpret_cast<const uint16_t*>(wire[b].data_ptr()),
+                             f.data_ptr<float>(), f.numel(), scale, cs);
+      } else {
+        comm->all_reduce_raw(f.data_ptr(), (size_t)f.numel(), RcclComm::dtype_of(f),
+                             average ? ncclAvg : ncclSum);
+      }
+    } else {
+      py::gil_scoped_acquire gil;
+      py_launch(b);
+    }
+  }
+
+  void launch_ready_in_order() {
+    while (next_launch < (int64_t)flats.size() && bucket_ready[next_launch]) {
+      launch_bucket(next_launch);
+      ++next_launch;
+    }
+  }
+
+  void mark_param(int64_t idx, bool zero_if_missing) {
+    if (param_ready[idx]) return;
+    param_ready[idx] = 1;
+    at::Tensor& p = params[idx];
+    const at::Tensor& v = views[idx];
+    at::Tensor& g = p.mutable_grad();
+    if (g.defined()) {
+      if (g.data_ptr() != v.data_ptr() || g.strides() != v.strides()) {
+        v.copy_(g);
+        g = v;
+      }
+    } else if (zero_if_missing) {
+      v.zero_();
+      g = v;
+    }
+    int64_t b = bucket_of[idx];
+    if (--pending[b] == 0) {
+      bucket_ready[b] = 1;
+      launch_ready_in_order();
+    }
+  }
+
+  void finalize() {
+    std::lock_guard<std::mutex> lk(mu);
+    // parameters that received no gradient this iteration (unused in forward): zero views
+    for (size_t i = 0; i < params.size(); ++i)
+      if (!param_ready[i]) mark_param((int64_t)i, /*zero_if_missing=*/true);
+    if (comm) {
+      comm->current_wait_comm();
+    } else {
+      py::gil_scoped_acquire gil;
+      py_finalize();
+    }
+    last_order = launch_order;
+    expecting = false;
+    callback_queued = false;
+    ++iters;
+  }
+};
+
+Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
+                 std::vector<int64_t> bucket_of_param, std::vector<at::Tensor> bucket_flats,
+                 std::shared_ptr<RcclComm> comm, py::object py_launch, py::object py_finalize,
+                 bool average, std::string wire_dtype)
+    : st_(std::make_shared<ReducerState>()) {
+  if (params.size() != grad_views.size() || params.size() != bucket_of_param.size())
+    throw std::runtime_error("Reducer: params/views/bucket_of size mismatch");
+  st_->params = std::move(params);
+  st_->views = std::move(grad_views);
+  st_->bucket_of = std::move(bucket_of_param);
+  st_->flats = std::move(bucket_flats);
+  st_->comm = std::move(comm);
+  st_->py_launch = std::move(py_launch);
+  st_->py_finalize = std::move(py_finalize);
+  st_->average = average;
+  st_->wire_bf16 = (wire_dtype == "bf16");
+  if (st_->wire_bf16 && !st_->comm) throw std::runtime_error("bf16 wire format needs the RCCL comm");
+  st_->wire.resize(st_->flats.size());
+  st_->members.resize(st_->flats.size());
+  for (size_t i = 0; i < st_->params.size(); ++i) {
+    int64_t b = st_->bucket_of[i];
+    if (b < 0 || b >= (int64_t)st_->flats.size()) throw std::runtime_error("Reducer: bad bucket id");
+    st_->members[b].push_back((int64_t)i);
+  }
+  st_->reset_counters();
+
+  std::weak_ptr<ReducerState> weak = st_;
+  for (size_t i = 0; i < st_->params.size(); ++i) {
+    auto acc = torch::autograd::impl::grad_accumulator(st_->params[i]);
+    if (!acc) throw std::runtime_error("Reducer: parameter has no grad accumulator (requires_grad?)");
+    int64_t idx = (int64_t)i;
+    acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+        [weak, idx](const torch::autograd::variable_list& outputs,
+                    const torch::autograd::variable_list& /*inputs*/) {
+          auto s = weak.lock();
+          if (!s) return outputs;
+          std::lock_guard<std::mutex> lk(s->mu);
+          if (!s->enabled || !s->expecting) return outputs;
+          if (!s->callback_queued) {
+            s->callback_queued = true;
+            std::weak_ptr<ReducerState> w2 = s;
+            torch::autograd::Engine::get_default_engine().queue_callback([w2]() {
+              if (auto s2 = w2.lock()) s2->finalize();
+            });
+          }
+          s->mark_param(idx, /*zero_if_missing=*/false);
+          return outputs;
+        }));
+    st_->accumulators.push_back(std::move(acc));
+  }
+}
+
+Reducer::~Reducer() = default;
+
+void Reducer::prepare_for_backward() {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  st_->reset_counters();
+  st_->expecting = st_->enabled;
+  st_->callback_queued = false;
+}
+
+void Reducer::set_enabled(bool enabled) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  st_->enabled = enabled;
+}
+
+bool Reducer::enabled() const { return st_->enabled; }
+int64_t Reducer::num_buckets() const { return (int64_t)st_->flats.size(); }
+std::vector<int64_t> Reducer::last_launch_order() const { return st_->last_order; }
+int64_t Reducer::iterations() const { return st_->iters; }
+
+}  // namespace pdt

@@ -1,0 +1,56 @@
+// Native gradient reducer for data-parallel training.
+//
+// Plays the role of c10d's C++ Reducer that DistributedDataParallel creates at
+// torch/nn/parallel/distributed.py:1227 (reference resnet/main.py:80), designed
+// for the MI355X path:
+//   * every parameter's .grad is a view into ONE flat fp32 gradient buffer,
+//     partitioned into buckets in reverse-definition (= grad-ready) order, so a
+//     bucket all-reduce is a single contiguous RCCL call and the optimizer can
+//     run one fused kernel over the whole flat buffer;
+//   * an autograd post-hook on each parameter's AccumulateGrad node marks it
+//     ready (copying the grad into its view only when autograd did not already
+//     accumulate in place); a full bucket is launched immediately -- in bucket
+//     order, as collectives must be issued identically on every rank -- on the
+//     RCCL comm stream behind an event, so the all-reduce overlaps the rest of
+//     backward;
+//   * averaging is folded into the collective (ncclAvg), optionally with bf16
+//     wire format (halves xGMI bytes) cast back into the fp32 buffer;
+//   * a final autograd callback makes the caller's stream wait for the comm
+//     stream, zero-fills buckets of parameters that got no gradient, and resets.
+// Non-RCCL process groups (gloo on CPU, used by the tests) plug in via Python
+// launch/finalize callbacks while keeping all the bookkeeping here.
+#pragma once
+#include <ATen/ATen.h>
+#include <pybind11/pybind11.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../comm/rccl_comm.h"
+
+namespace pdt {
+
+struct ReducerState;
+
+class Reducer {
+ public:
+  Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
+          std::vector<int64_t> bucket_of_param, std::vector<at::Tensor> bucket_flats,
+          std::shared_ptr<RcclComm> comm, pybind11::object py_launch,
+          pybind11::object py_finalize, bool average, std::string wire_dtype);
+  ~Reducer();
+
+  void prepare_for_backward();
+  void set_enabled(bool enabled);
+  bool enabled() const;
+  int64_t num_buckets() const;
+  std::vector<int64_t> last_launch_order() const;
+  int64_t iterations() const;
+
+ private:
+  std::shared_ptr<ReducerState> st_;
+};
+
+}  // namespace pdt

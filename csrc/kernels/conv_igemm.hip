@@ -1,0 +1,734 @@
+// Implicit-GEMM convolution for gfx950 (MI355X / CDNA4): forward, data-gradient
+// and weight-gradient, NHWC bf16 in, fp32 MFMA accumulation.
+//
+// Why implicit GEMM on MFMA: every ResNet conv is GEMM-shaped
+// (SURVEY.md §2.6): fwd M=N*Ho*Wo, N=K, K=R*S*C; dgrad M=N*H*W, N=C,
+// K=K*R*S; wgrad M=K, N=R*S*C, K=N*Ho*Wo.  The im2col matrix is never
+// materialised: the A-tile loader gathers 16-byte (8-channel) NHWC vectors
+// straight from the activation with bounds-checked buffer loads (padding reads
+// return 0 from the buffer unit's range check -- no branches, no zero fill),
+// stages them in LDS with an XOR swizzle that makes the MFMA fragment reads
+// bank-conflict free, and the waves run v_mfma_f32_16x16x32_bf16.
+//
+// Kernel families
+//   igemm_nt : A rows k-contiguous (gathered activations), B rows k-contiguous
+//              (packed weights).  fwd: B = W[K][R][S][C].  dgrad: A = dy,
+//              B = W^T[C][R][S][K]; stride > 1 is split into stride^2 parity
+//              classes (one launch each) so no MFMA work is spent on the
+//              structural zeros of the transposed convolution.  The fwd
+//              epilogue also emits BatchNorm partial statistics (sum and M2 per
+//              16*TM-row group per channel) from the fp32 accumulators, so BN
+//              never re-reads the conv output to compute its batch stats.
+//   igemm_tn : wgrad.  Both operands have the reduction index (pixels) as the
+//              strided dimension, so tiles are staged [m][col] and fragments are
+//              read with the CDNA4 transposing LDS read ds_read_b64_tr_b16.
+//              Long reductions (up to 3.2M pixels) are split-K over blockIdx.z
+//              into an fp32 slab reduced by a second deterministic pass.
+//
+// Pipeline (both): 4 waves, BK = 64, two LDS buffers, register-staged prefetch
+// of tile k+1 issued before the MFMAs of tile k and written to LDS after them,
+// one barrier per K-step.  Block ids are remapped so consecutive tiles (sharing
+// the A panel) run on the same XCD and hit its L2.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace pdt {
+
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+
+// ---------------------------------------------------------------- utilities
+struct FastDiv {  // n / d for 0 <= n < 2^31 via mul-hi
+  uint32_t mul, shr;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shr = l;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t hi = __umulhi(n, f.mul);
+  return (hi + n) >> f.shr;
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // bijective: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get consecutive ids
+  int q = nwg / 8, r = nwg % 8;
+  int xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ v4i buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ v4f mfma16(const v4i& a, const v4i& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a),
+                                                __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
+}
+
+constexpr uint32_t OOB = 0x80000000u;  // any offset >= num_records reads 0
+
+// ============================================================================
+//                          NT implicit GEMM (fwd / dgrad)
+// ============================================================================
+constexpr int MAX_TAPS = 49;
+
+struct NtArgs {
+  const uint16_t* a;   // activation source NHWC (x for fwd, dy for dgrad), CA channels
+  const uint16_t* b;   // [Nout][Kg] k-contiguous
+  uint16_t* out;       // NHWC output, Nout channels
+  float* part;         // BN partials [ngroups][2][Nout] or null
+  uint32_t a_bytes, b_bytes;
+  int HA, WA, CA;      // A source dims
+  int Nout, Kg, S;     // GEMM N, B row length (= taps_total*CA), filter width (generic path)
+  int M;               // GEMM rows of this launch
+  FastDiv div_ij, div_j;  // m -> n = m / Mij, i = rem / Mj
+  int Mij, Mj;
+  int ash, asw, aoff_h, aoff_w;     // A base coords: h0 = i*ash + aoff_h
+  int OH, OW, osh, osw, oph, opw;   // out row = (n*OH + i*osh + oph)*OW + j*osw + opw
+  int ntaps;
+  int8_t tdr[MAX_TAPS], tds[MAX_TAPS];
+  int16_t tb[MAX_TAPS];
+};
+
+// LDS image of a [rows][64] bf16 tile: 128-B rows, 16-B chunk XOR-swizzled by (row>>1)&7.
+// For the 16x16x32 fragment read (lane l: row l&15, chunk 4*ksub + (l>>4)) every ds_read_b128
+// lane group then touches 16 distinct 16-B slots of the 256-B bank row: conflict-free.
+__device__ __forceinline__ int swz128(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+template <int WM, int WN, int TM, int TN>
+struct NtCfg {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * TM * 16;
+  static constexpr int BN = WN * TN * 16;
+  static constexpr int A_PT = BM * 8 / NT;  // 16-B chunks per thread (8 chunks per 64-wide row)
+  static constexpr int B_PT = BN * 8 / NT;
+  static constexpr int ROWSTEP = NT / 8;
+  static constexpr int PIPE_BYTES = 2 * (BM + BN) * 128;
+  static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row
+  static constexpr int EPI_BYTES = WM * WN * (TM * 16) * EPI_PITCH;
+  static constexpr int SMEM = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
+};
+
+template <int WM, int WN, int TM, int TN, bool C64, bool STATS>
+__global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) {
+  using CFG = NtCfg<WM, WN, TM, TN>;
+  constexpr int BM = CFG::BM, BN = CFG::BN;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntn = (P.Nout + BN - 1) / BN;
+  const int ntm = (P.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
+  const int m0 = tmi * BM, n0 = tni * BN;
+
+  const int t = threadIdx.x;
+  const int cc = t & 7;
+  const int rbase = t >> 3;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
+
+  int a_pix[CFG::A_PT], a_h0[CFG::A_PT], a_w0[CFG::A_PT];
+#pragma unroll
+  for (int i = 0; i < CFG::A_PT; ++i) {
+    int m = m0 + rbase + CFG::ROWSTEP * i;
+    if (m < P.M) {
+      uint32_t n = fdiv((uint32_t)m, P.div_ij);
+      uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+      uint32_t ii = fdiv(rem, P.div_j);
+      uint32_t jj = rem - ii * (uint32_t)P.Mj;
+      a_pix[i] = (int)n * P.HA * P.WA;
+      a_h0[i] = (int)ii * P.ash + P.aoff_h;
+      a_w0[i] = (int)jj * P.asw + P.aoff_w;
+    } else {
+      a_pix[i] = 0; a_h0[i] = -(1 << 20); a_w0[i] = 0;
+    }
+  }
+  int b_row[CFG::B_PT];
+#pragma unroll
+  for (int i = 0; i < CFG::B_PT; ++i) {
+    int n = n0 + rbase + CFG::ROWSTEP * i;
+    b_row[i] = n < P.Nout ? n * P.Kg : -1;
+  }
+
+  const int cb = P.CA >> 6;
+  const int nk = C64 ? P.ntaps * cb : (P.Kg + 63) / 64;
+
+  v4i ra_reg[CFG::A_PT], rb_reg[CFG::B_PT];
+
+  auto load_tiles = [&](int kt) {
+    if constexpr (C64) {
+      const int tap = kt / cb;
+      const int ch = (kt - tap * cb) * 64 + cc * 8;
+      const int dr = P.tdr[tap], ds = P.tds[tap];
+      const int tbo = (int)P.tb[tap] * P.CA + ch;
+#pragma unroll
+      for (int i = 0; i < CFG::A_PT; ++i) {
+        int h = a_h0[i] + dr, w = a_w0[i] + ds;
+        bool ok = (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
+        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * 2) : OOB;
+        ra_reg[i] = buf_load16(ra, off);
+      }
+#pragma unroll
+      for (int i = 0; i < CFG::B_PT; ++i) {
+        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * 2) : OOB;
+        rb_reg[i] = buf_load16(rb, off);
+      }
+    } else {
+      const int kk = kt * 64 + cc * 8;
+      const bool kok = kk < P.Kg;
+      const int tap = kk / P.CA;
+      const int ch = kk - tap * P.CA;
+      const int r = tap / P.S;
+      const int s = tap - r * P.S;
+#pragma unroll
+      for (int i = 0; i < CFG::A_PT; ++i) {
+        int h = a_h0[i] + r, w = a_w0[i] + s;
+        bool ok = kok && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
+        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * 2) : OOB;
+        ra_reg[i] = buf_load16(ra, off);
+      }
+#pragma unroll
+      for (int i = 0; i < CFG::B_PT; ++i) {
+        uint32_t off = (kok && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * 2) : OOB;
+        rb_reg[i] = buf_load16(rb, off);
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    char* As = smem + buf * (BM + BN) * 128;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int i = 0; i < CFG::A_PT; ++i)
+      *reinterpret_cast<v4i*>(As + swz128(rbase + CFG::ROWSTEP * i, cc)) = ra_reg[i];
+#pragma unroll
+    for (int i = 0; i < CFG::B_PT; ++i)
+      *reinterpret_cast<v4i*>(Bs + swz128(rbase + CFG::ROWSTEP * i, cc)) = rb_reg[i];
+  };
+
+  const int wid = t >> 6, lane = t & 63;
+  const int wm = wid % WM, wn = wid / WM;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_tiles(0);
+    store_tiles(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles(kt + 1);
+    const char* As = smem + cur * (BM + BN) * 128;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kc = ks * 4 + fq;
+      v4i af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int row = wm * TM * 16 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const v4i*>(As + swz128(row, kc));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int row = wn * TN * 16 + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(row, kc));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // --------------------------------------------------------------- epilogue
+  const int wrow0 = m0 + wm * TM * 16;  // first GEMM row of this wave
+  const int wcol0 = n0 + wn * TN * 16;
+
+  if constexpr (STATS) {
+    // per column: sum and M2 over this wave's TM*16 rows (valid rows only)
+    const int group = tmi * WM + wm;
+    const int valid = min(TM * 16, P.M - wrow0);
+    if (valid > 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int r = i * 16 + fq * 4 + e;
+            s += r < valid ? acc[i][j][e] : 0.f;
+          }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mu = s / (float)valid;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int r = i * 16 + fq * 4 + e;
+            float d = acc[i][j][e] - mu;
+            q += r < valid ? d * d : 0.f;
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        const int col = wcol0 + j * 16 + fr;
+        if (fq == 0 && col < P.Nout) {
+          P.part[((int64_t)group * 2 + 0) * P.Nout + col] = s;
+          P.part[((int64_t)group * 2 + 1) * P.Nout + col] = q;
+        }
+      }
+    }
+  }
+
+  // stage the wave's TM*16 x TN*16 tile as bf16 in LDS, then store 16-B row chunks
+  char* ep = smem + wid * (TM * 16) * CFG::EPI_PITCH;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int r = i * 16 + fq * 4 + e;
+        int c = j * 16 + fr;
+        *reinterpret_cast<uint16_t*>(ep + r * CFG::EPI_PITCH + c * 2) = f2bf(acc[i][j][e]);
+      }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private region, no barrier needed
+  __builtin_amdgcn_wave_barrier();
+  constexpr int CH_PER_ROW = TN * 2;  // 16-B chunks per wave-tile row
+  constexpr int CHUNKS = TM * 16 * CH_PER_ROW;
+#pragma unroll
+  for (int q = lane; q < CHUNKS; q += 64) {
+    int r = q / CH_PER_ROW, c = q - r * CH_PER_ROW;
+    int m = wrow0 + r;
+    int col = wcol0 + c * 8;
+    if (m < P.M && col < P.Nout) {
+      uint32_t n = fdiv((uint32_t)m, P.div_ij);
+      uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+      uint32_t ii = fdiv(rem, P.div_j);
+      uint32_t jj = rem - ii * (uint32_t)P.Mj;
+      int64_t orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+      *reinterpret_cast<v4i*>(P.out + orow * P.Nout + col) =
+          *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+    }
+  }
+}
+
+// ============================================================================
+//                      TN implicit GEMM (wgrad, split-K)
+// ============================================================================
+struct TnArgs {
+  const uint16_t* dy;  // [Mred][Kout]
+  const uint16_t* x;   // [N][H][W][C]
+  float* out;          // [splits][Kout][Ncols] (or dw directly when splits == 1)
+  uint32_t dy_bytes, x_bytes;
+  int Mred, Kout, Ncols;
+  int H, W, C, S, stride, pad;
+  FastDiv div_hw, div_w;  // m -> n = m / (Ho*Wo), ho = rem / Wo
+  int HoWo, Wo;
+  int steps_per_split, nsteps;
+};
+
+// LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
+// swz(m)<<1 with swz(m) = (m&3) | ((m>>3)&1)<<2.  The transposing fragment read
+// (ds_read_b64_tr_b16: per 32-lane half, rows {m..m+3, m+8..m+11} x 32 B) then hits
+// 8 distinct 32-B bank windows: conflict-free; ds_write_b128 groups stay in one half-row.
+__device__ __forceinline__ int swz256(int row, int chunk) {
+  int sw = (row & 3) | (((row >> 3) & 1) << 2);
+  return row * 256 + ((chunk ^ (sw << 1)) << 4);
+}
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s_t ds_read_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s_t*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+__device__ __forceinline__ v4i cat_frag(v4s_t lo, v4s_t hi) {
+  return __builtin_bit_cast(v4i, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int BMG, int BNG>
+struct TnCfg {
+  static constexpr int NT = 256;
+  static constexpr int A_PT = 64 * (BMG / 8) / NT;   // chunks per thread
+  static constexpr int B_PT = 64 * (BNG / 8) / NT;
+  static constexpr int TILE_BYTES = 64 * 256;        // one [64][<=128] tile, 256-B pitch
+  static constexpr int SMEM = 2 * 2 * TILE_BYTES;    // 2 buffers x (A, B)
+  static constexpr int TM = BMG / 2 / 16;            // 2x2 waves
+  static constexpr int TN = BNG / 2 / 16;
+};
+
+template <int BMG, int BNG, bool C64>
+__global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
+  using CFG = TnCfg<BMG, BNG>;
+  constexpr int TM = CFG::TM, TN = CFG::TN;
+  constexpr int ACH = BMG / 8, BCH = BNG / 8;  // chunks per LDS row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntn = (P.Ncols + BNG - 1) / BNG;
+  const int ntm = (P.Kout + BMG - 1) / BMG;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
+  const int k0 = tmi * BMG, c0 = tni * BNG;
+  const int split = blockIdx.y;
+  const int s_begin = split * P.steps_per_split;
+  const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
+
+  const int t = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
+
+  // A chunks: q = t + 256 i -> m-row q / ACH, chunk q % ACH (fixed kout columns per thread)
+  const int a_c = t % ACH;
+  const int a_r = t / ACH;
+  constexpr int A_RSTEP = 256 / ACH;
+  const int a_col = k0 + a_c * 8;
+  const bool a_colok = a_col < P.Kout;
+  // B chunks: fixed column chunk per thread -> fixed (tap, channel)
+  const int b_c = t % BCH;
+  const int b_r = t / BCH;
+  constexpr int B_RSTEP = 256 / BCH;
+  const int b_col = c0 + b_c * 8;
+  const bool b_colok = b_col < P.Ncols;
+  int b_tr = 0, b_ts = 0, b_ch = 0;
+  {
+    int tap = b_col / P.C;
+    b_ch = b_col - tap * P.C;
+    b_tr = tap / P.S;
+    b_ts = tap - b_tr * P.S;
+  }
+  const int b_dh = b_tr - P.pad, b_dw = b_ts - P.pad;
+
+  v4i ra_reg[CFG::A_PT], rb_reg[CFG::B_PT];
+  auto load_tiles = [&](int step) {
+    const int mb = step * 64;
+#pragma unroll
+    for (int i = 0; i < CFG::A_PT; ++i) {
+      int m = mb + a_r + A_RSTEP * i;
+      bool ok = a_colok && m < P.Mred;
+      uint32_t off = ok ? (uint32_t)(((int64_t)m * P.Kout + a_col) * 2) : OOB;
+      ra_reg[i] = buf_load16(rdy, off);
+    }
+#pragma unroll
+    for (int i = 0; i < CFG::B_PT; ++i) {
+      int m = mb + b_r + B_RSTEP * i;
+      uint32_t off = OOB;
+      if (b_colok && m < P.Mred) {
+        uint32_t n = fdiv((uint32_t)m, P.div_hw);
+        uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
+        uint32_t ho = fdiv(rem, P.div_w);
+        uint32_t wo = rem - ho * (uint32_t)P.Wo;
+        int h = (int)ho * P.stride + b_dh, w = (int)wo * P.stride + b_dw;
+        if ((unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W)
+          off = (uint32_t)(((((int)n * P.H + h) * P.W + w) * P.C + b_ch) * 2);
+      }
+      rb_reg[i] = buf_load16(rx, off);
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    char* As = smem + buf * 2 * CFG::TILE_BYTES;
+    char* Bs = As + CFG::TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < CFG::A_PT; ++i)
+      *reinterpret_cast<v4i*>(As + swz256(a_r + A_RSTEP * i, a_c)) = ra_reg[i];
+#pragma unroll
+    for (int i = 0; i < CFG::B_PT; ++i)
+      *reinterpret_cast<v4i*>(Bs + swz256(b_r + B_RSTEP * i, b_c)) = rb_reg[i];
+  };
+
+  const int wid = t >> 6, lane = t & 63;
+  const int wm = wid & 1, wn = wid >> 1;
+  const int li = lane & 15, g = lane >> 4;  // group g covers k rows 8g..8g+7
+  // tr-read address pieces: lane 4q+p of a group -> row q, columns 4p..4p+3
+  const int tq = li >> 2, tp = li & 3;
+
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  auto frag_addr = [&](const char* base, int row, int col) -> const char* {
+    // col multiple of 4; chunk = col/8, byte-in-chunk = (col%8)*2
+    return base + swz256(row, col >> 3) + ((col & 7) << 1);
+  };
+
+  if (s_begin < s_end) {
+    load_tiles(s_begin);
+    store_tiles(0);
+  }
+  __syncthreads();
+  for (int step = s_begin; step < s_end; ++step) {
+    const int cur = (step - s_begin) & 1;
+    if (step + 1 < s_end) load_tiles(step + 1);
+    const char* As = smem + cur * 2 * CFG::TILE_BYTES;
+    const char* Bs = As + CFG::TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int rowA = ks * 32 + 8 * g + tq;  // m row of the first tr block
+      v4i af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int col = wm * TM * 16 + i * 16 + 4 * tp;
+        v4s_t lo = ds_read_tr(frag_addr(As, rowA, col));
+        v4s_t hi = ds_read_tr(frag_addr(As, rowA + 4, col));
+        af[i] = cat_frag(lo, hi);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int col = wn * TN * 16 + j * 16 + 4 * tp;
+        v4s_t lo = ds_read_tr(frag_addr(Bs, rowA, col));
+        v4s_t hi = ds_read_tr(frag_addr(Bs, rowA + 4, col));
+        bfr[j] = cat_frag(lo, hi);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (step + 1 < s_end) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: fp32 [Kout][Ncols] slab of this split; lane holds rows fq*4+e, column fr
+  const int fq = lane >> 4, fr = lane & 15;
+  float* o = P.out + (int64_t)split * P.Kout * P.Ncols;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int col = c0 + wn * TN * 16 + j * 16 + fr;
+      if (col >= P.Ncols) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int row = k0 + wm * TM * 16 + i * 16 + fq * 4 + e;
+        if (row < P.Kout) o[(int64_t)row * P.Ncols + col] = acc[i][j][e];
+      }
+    }
+}
+
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                            int64_t n, float* __restrict__ out) {
+  int64_t n4 = n / 4;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(ws)[i];
+    for (int k = 1; k < splits; ++k) {
+      float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(int64_t)k * n + i];
+    out[i] = s;
+  }
+}
+
+// ============================================================================
+//                                   host side
+// ============================================================================
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <int WM, int WN, int TM, int TN, bool C64, bool STATS>
+static void run_nt(const NtArgs& a, hipStream_t st) {
+  using CFG = NtCfg<WM, WN, TM, TN>;
+  int ntm = (a.M + CFG::BM - 1) / CFG::BM;
+  int ntn = (a.Nout + CFG::BN - 1) / CFG::BN;
+  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, C64, STATS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), CFG::SMEM, st, a);
+  check_launch("igemm_nt");
+}
+
+// tile choice: output channels 64 -> tall tile (more M rows per block); small M -> short tile
+template <bool C64, bool STATS>
+static void dispatch_nt(const NtArgs& a, hipStream_t st, int* group_rows) {
+  if (a.Nout <= 64) {
+    if (group_rows) *group_rows = 64;
+    run_nt<4, 1, 4, 4, C64, STATS>(a, st);       // 256 x 64
+  } else if (a.M <= 8192) {
+    if (group_rows) *group_rows = 32;
+    run_nt<2, 2, 2, 4, C64, STATS>(a, st);       // 64 x 128
+  } else {
+    if (group_rows) *group_rows = 64;
+    run_nt<2, 2, 4, 4, C64, STATS>(a, st);       // 128 x 128
+  }
+}
+
+int conv_fwd_group_rows(int M, int Nout) { return Nout <= 64 ? 64 : (M <= 8192 ? 32 : 64); }
+
+static void fill_common(NtArgs& a, int Mi, int Mj) {
+  a.Mij = Mi * Mj;
+  a.Mj = Mj;
+  a.div_ij = make_fastdiv((uint32_t)a.Mij);
+  a.div_j = make_fastdiv((uint32_t)Mj);
+}
+
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
+                     const ConvShape& s, hipStream_t st) {
+  NtArgs a{};
+  a.a = x; a.b = w; a.out = y; a.part = part;
+  a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
+  a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C * 2);
+  a.HA = s.H; a.WA = s.W; a.CA = s.C;
+  a.Nout = s.K; a.Kg = s.R * s.S * s.C; a.S = s.S;
+  a.M = s.N * s.Ho * s.Wo;
+  fill_common(a, s.Ho, s.Wo);
+  a.ash = s.stride; a.asw = s.stride; a.aoff_h = -s.pad; a.aoff_w = -s.pad;
+  a.OH = s.Ho; a.OW = s.Wo; a.osh = 1; a.osw = 1; a.oph = 0; a.opw = 0;
+  a.ntaps = s.R * s.S;
+  if (a.ntaps > MAX_TAPS) throw std::runtime_error("conv_fwd: too many taps");
+  for (int r = 0; r < s.R; ++r)
+    for (int q = 0; q < s.S; ++q) {
+      int i = r * s.S + q;
+      a.tdr[i] = (int8_t)r; a.tds[i] = (int8_t)q; a.tb[i] = (int16_t)i;
+    }
+  bool c64 = (s.C % 64) == 0;
+  if (part) {
+    if (c64) dispatch_nt<true, true>(a, st, nullptr);
+    else dispatch_nt<false, true>(a, st, nullptr);
+  } else {
+    if (c64) dispatch_nt<true, false>(a, st, nullptr);
+    else dispatch_nt<false, false>(a, st, nullptr);
+  }
+}
+
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvShape& s,
+                       hipStream_t st) {
+  if (s.K % 64 != 0) throw std::runtime_error("conv_dgrad: output channels must be a multiple of 64");
+  const int str = s.stride;
+  for (int ph = 0; ph < str; ++ph)
+    for (int pw = 0; pw < str; ++pw) {
+      NtArgs a{};
+      a.a = dy; a.b = wt; a.out = dx; a.part = nullptr;
+      a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
+      a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * 2);
+      a.HA = s.Ho; a.WA = s.Wo; a.CA = s.K;
+      a.Nout = s.C; a.Kg = s.R * s.S * s.K; a.S = s.S;
+      const int Mi = (s.H - ph + str - 1) / str;
+      const int Mj = (s.W - pw + str - 1) / str;
+      if (Mi <= 0 || Mj <= 0) continue;
+      a.M = s.N * Mi * Mj;
+      fill_common(a, Mi, Mj);
+      a.ash = 1; a.asw = 1; a.aoff_h = 0; a.aoff_w = 0;
+      a.OH = s.H; a.OW = s.W; a.osh = str; a.osw = str; a.oph = ph; a.opw = pw;
+      // taps of this parity class: (ph + pad - r) % str == 0 -> ho = i + (ph + pad - r)/str
+      int nt = 0;
+      for (int r = 0; r < s.R; ++r) {
+        int dh = ph + s.pad - r;
+        if (((dh % str) + str) % str != 0) continue;
+        for (int q = 0; q < s.S; ++q) {
+          int dw = pw + s.pad - q;
+          if (((dw % str) + str) % str != 0) continue;
+          a.tdr[nt] = (int8_t)(dh >= 0 ? dh / str : -((-dh) / str));
+          a.tds[nt] = (int8_t)(dw >= 0 ? dw / str : -((-dw) / str));
+          a.tb[nt] = (int16_t)(r * s.S + q);
+          ++nt;
+        }
+      }
+      a.ntaps = nt;  // nt == 0 -> kernel writes zeros for this class
+      dispatch_nt<true, false>(a, st, nullptr);
+    }
+}
+
+// ------------------------------------------------------------------- wgrad
+struct WgradPlan {
+  int bmg, bng, tiles, splits, steps_per_split, nsteps;
+};
+
+static WgradPlan plan_wgrad(const ConvShape& s) {
+  WgradPlan p;
+  p.bmg = s.K <= 64 ? 64 : 128;
+  p.bng = 128;
+  const int ncols = s.R * s.S * s.C;
+  p.tiles = ((s.K + p.bmg - 1) / p.bmg) * ((ncols + p.bng - 1) / p.bng);
+  const int64_t mred = (int64_t)s.N * s.Ho * s.Wo;
+  p.nsteps = (int)((mred + 63) / 64);
+  int target = 1024;  // ~4 blocks per CU
+  int splits = (target + p.tiles - 1) / p.tiles;
+  splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
+  splits = std::max(1, std::min(splits, 256));
+  p.steps_per_split = (p.nsteps + splits - 1) / splits;
+  p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
+  return p;
+}
+
+size_t conv_wgrad_ws_floats(const ConvShape& s) {
+  WgradPlan p = plan_wgrad(s);
+  if (p.splits <= 1) return 0;
+  return (size_t)p.splits * s.K * s.R * s.S * s.C;
+}
+
+template <int BMG, int BNG>
+static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
+  using CFG = TnCfg<BMG, BNG>;
+  auto kfn = igemm_tn_kernel<BMG, BNG, true>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(tiles, splits), dim3(256), CFG::SMEM, st, a);
+  check_launch("igemm_tn");
+}
+
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
+                       const ConvShape& s, hipStream_t st) {
+  if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
+  WgradPlan p = plan_wgrad(s);
+  TnArgs a{};
+  a.dy = dy; a.x = x;
+  a.out = p.splits > 1 ? ws : dw;
+  a.dy_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
+  a.x_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
+  a.Mred = s.N * s.Ho * s.Wo; a.Kout = s.K; a.Ncols = s.R * s.S * s.C;
+  a.H = s.H; a.W = s.W; a.C = s.C; a.S = s.S; a.stride = s.stride; a.pad = s.pad;
+  a.HoWo = s.Ho * s.Wo; a.Wo = s.Wo;
+  a.div_hw = make_fastdiv((uint32_t)a.HoWo);
+  a.div_w = make_fastdiv((uint32_t)s.Wo);
+  a.steps_per_split = p.steps_per_split;
+  a.nsteps = p.nsteps;
+  if (p.bmg == 64) run_tn<64, 128>(a, p.tiles, p.splits, st);
+  else run_tn<128, 128>(a, p.tiles, p.splits, st);
+  if (p.splits > 1) {
+    int64_t n = (int64_t)s.K * a.Ncols;
+    int64_t b = (n / 4 + 255) / 256;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 4096))),
+                       dim3(256), 0, st, ws, p.splits, n, dw);
+    check_launch("splitk_reduce");
+  }
+}
+
+}  // namespace pdt

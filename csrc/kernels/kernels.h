@@ -1,0 +1,91 @@
+// Host-side launchers of the gfx950 kernels.  Plain C++ signatures (raw device
+// pointers + hipStream_t) so the .hip translation units compile without any
+// PyTorch headers; csrc/bindings.cpp adapts them to torch tensors.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdt {
+
+// ---------------------------------------------------------------- layout.hip
+// NCHW fp32 image -> NHWC bf16 padded to Cp channels (Cp % 8 == 0).
+void launch_image_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int W, int Cp,
+                          hipStream_t st);
+// fp32 weight [K][C][R][S] with arbitrary strides -> bf16 [K][R][S][Cp] (zero pad c >= C)
+void launch_pack_weight(const float* w, const int64_t* strides, uint16_t* out, int K, int C,
+                        int R, int S, int Cp, hipStream_t st);
+// fp32 weight [K][C][R][S] -> bf16 [C][R][S][K] (dgrad B operand; no flip, taps indexed explicitly)
+void launch_pack_weight_t(const float* w, const int64_t* strides, uint16_t* out, int K, int C,
+                          int R, int S, hipStream_t st);
+
+// ---------------------------------------------------------- conv_igemm.hip
+struct ConvShape {
+  int N, H, W, C;      // input activation (C = channel stride, multiple of 8)
+  int K, R, S;         // filter: K outputs, RxS taps
+  int Ho, Wo;          // output spatial
+  int stride, pad;
+};
+// y[N,Ho,Wo,K] = conv(x, w[K][R][S][C]); if part != nullptr also writes per-group
+// BN partials part[ceil(M/G)][2][K] = (sum, M2 about the group mean), G = conv_fwd_group_rows().
+int conv_fwd_group_rows(int M, int Nout);
+void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
+                     const ConvShape& s, hipStream_t st);
+// dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (all stride/pad combos, parity classes)
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvShape& s,
+                       hipStream_t st);
+// dw[K][R][S][C] (fp32) = wgrad(dy, x).  ws: fp32 workspace of conv_wgrad_ws_floats() floats.
+size_t conv_wgrad_ws_floats(const ConvShape& s);
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
+                       const ConvShape& s, hipStream_t st);
+
+// -------------------------------------------------------------- bn_act.hip
+// part[ngroups][2][K] (group g has min(grows, M-grows*g) rows) -> out[4][K] = mean, invstd,
+// scale, shift; updates running stats in place (unbiased var) when rm/rv non-null.
+// `out` must have room for 4*K + 3*K*bn_finalize_partitions(ngroups) floats (stage-1 scratch).
+int bn_finalize_partitions(int ngroups);
+void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K, float* rm, float* rv,
+                        const float* gamma, const float* beta, float momentum, float eps,
+                        float* out, hipStream_t st);
+void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma, const float* beta,
+                           float eps, int K, float* out, hipStream_t st);
+// z = act(y*scale + shift (+res))
+void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
+                       const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
+                       hipStream_t st);
+// sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * (z>0 if relu); ws >= bn_bwd_ws_floats
+size_t bn_bwd_ws_floats(int64_t M, int K);
+void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
+                              const float* mean, bool relu, int64_t M, int K, float* ws,
+                              float* sums, hipStream_t st);
+// dy = gamma*invstd*(g - sum_g/M - xhat*sum_gx*invstd/M) (training) / gamma*invstd*g (eval);
+// dres = g (if non-null)
+void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
+                             const float* mean, const float* invstd, const float* gamma,
+                             const float* sums, bool relu, bool training, int64_t M, int K,
+                             uint16_t* dy, uint16_t* dres, hipStream_t st);
+
+// ---------------------------------------------------------------- pool.hip
+void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                        int Ho, int Wo, hipStream_t st);
+void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, hipStream_t st);
+void launch_avgpool_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st);
+void launch_avgpool_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+
+// ---------------------------------------------------------------- head.hip
+// loss[0] = mean CE, dlogits = (softmax - onehot)/N ; ws >= N floats
+void launch_softmax_xent(const float* logits, const int64_t* labels, float* loss, float* dlogits,
+                         float* ws, int N, int V, hipStream_t st);
+void launch_top1(const float* logits, const int64_t* labels, int64_t* count, int N, int V,
+                 hipStream_t st);
+
+// ----------------------------------------------------------------- sgd.hip
+// torch.optim.SGD on flat fp32 buffers; grad is scaled by grad_scale first.
+void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
+                float dampening, float wd, bool nesterov, bool first, float grad_scale,
+                hipStream_t st);
+// fp32 -> bf16 cast (used for bf16 gradient buckets) and back
+void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
+void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t st);
+
+}  // namespace pdt

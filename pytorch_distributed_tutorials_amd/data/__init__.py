@@ -1,0 +1,10 @@
+from .datasets import (  # noqa: F401
+    CIFAR_MEAN,
+    CIFAR_STD,
+    TensorImageDataset,
+    build_dataset,
+    cifar10,
+    synthetic_dataset,
+)
+from .loader import DeviceLoader, random_crop_flip  # noqa: F401
+from .sampler import DistributedSampler  # noqa: F401

@@ -1,0 +1,18 @@
+"""Ops layer: fused ResNet ops backed by hand-written HIP kernels.
+
+See ``fused.py`` for the autograd units and ``reference.py`` for the PyTorch
+semantics they implement.  ``native_available()`` reports whether the gfx950
+extension loaded.
+"""
+from ._ext import native, native_available  # noqa: F401
+from .fused import (  # noqa: F401
+    CrossEntropyLoss,
+    act_dtype,
+    avgpool_linear,
+    conv_bn,
+    cross_entropy,
+    image_to_nhwc,
+    maxpool3x3s2,
+    set_cpu_activation_dtype,
+    top1_correct,
+)

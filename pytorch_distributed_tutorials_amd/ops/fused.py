@@ -1,0 +1,231 @@
+"""Fused ResNet building blocks as autograd Functions.
+
+Each function dispatches on the device of its input:
+  * device tensor -> the HIP kernels of the native extension (``_C``); a missing
+    extension raises (``_ext.native()``), never silently falls back;
+  * CPU tensor    -> ``ops.reference`` (PyTorch), which defines the semantics.
+
+The unit of fusion is ``conv -> BatchNorm(batch stats) -> (+residual) -> ReLU``
+(SURVEY.md §3.5 fusion points).  Forward launches: weight pack, implicit-GEMM
+conv with per-tile BN partial statistics in its epilogue, a tiny stats
+finalize (which also updates the running buffers), one fused
+normalize/add/ReLU pass.  Backward: one reduction pass (dgamma, dbeta), one
+elementwise pass producing dy (and the residual-branch gradient), then the
+dgrad and wgrad implicit GEMMs.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import reference as ref
+from ._ext import native
+
+_CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
+
+
+def set_cpu_activation_dtype(dtype: torch.dtype) -> None:
+    global _CPU_DTYPE
+    _CPU_DTYPE = dtype
+
+
+def act_dtype(device: torch.device) -> torch.dtype:
+    return torch.bfloat16 if device.type == "cuda" else _CPU_DTYPE
+
+
+# ----------------------------------------------------------------------------
+# image -> NHWC
+# ----------------------------------------------------------------------------
+def image_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """NCHW float image -> NHWC activation with C padded to 8 (no grad needed)."""
+    if x.is_cuda:
+        return native().image_to_nhwc(x.contiguous())
+    return ref.image_to_nhwc(x, _CPU_DTYPE)
+
+
+# ----------------------------------------------------------------------------
+# conv + BN + (residual) + ReLU
+# ----------------------------------------------------------------------------
+class _ConvBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, residual, running_mean, running_var,
+                stride, pad, relu, training, momentum, eps):
+        k, c, r, s = weight.shape
+        n, h, w, cx = x.shape
+        count = n * ((h + 2 * pad - r) // stride + 1) * ((w + 2 * pad - s) // stride + 1)
+        if x.is_cuda:
+            C = native()
+            wk = C.pack_weight(weight, cx)                       # bf16 [K,R,S,Cx]
+            y, part = C.conv_fwd(x, wk, stride, pad, training)    # bf16 NHWC + tile stats
+            if training:
+                if running_mean is None:  # track_running_stats=False: updates go to scratch
+                    running_mean = torch.zeros(k, device=x.device)
+                    running_var = torch.ones(k, device=x.device)
+                stats = C.bn_finalize(part, count, running_mean, running_var,
+                                      gamma, beta, float(momentum), float(eps))
+            else:
+                stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
+            mean, invstd, scale, shift = stats.unbind(0)
+            z = C.bn_act_fwd(y, scale, shift, residual, relu)
+        else:
+            wk = None
+            y = ref.conv2d_nhwc(x, weight, stride, pad).to(x.dtype)
+            if training:
+                mean, var = ref.bn_batch_stats(y)
+                with torch.no_grad():
+                    unbiased = var * count / max(count - 1, 1)
+                    running_mean.mul_(1 - momentum).add_(mean, alpha=momentum)
+                    running_var.mul_(1 - momentum).add_(unbiased, alpha=momentum)
+            else:
+                mean, var = running_mean.float(), running_var.float()
+            invstd = torch.rsqrt(var + eps)
+            z = ref.bn_act_fwd(y, mean, invstd, gamma, beta, residual, relu, x.dtype)
+        ctx.save_for_backward(x, weight, wk, y, z, mean, invstd, gamma)
+        ctx.cfg = (stride, pad, relu, training, residual is not None)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, weight, wk, y, z, mean, invstd, gamma = ctx.saved_tensors
+        stride, pad, relu, training, has_res = ctx.cfg
+        dz = dz.contiguous()
+        need_x = ctx.needs_input_grad[0]
+        need_w = ctx.needs_input_grad[1]
+        if dz.is_cuda:
+            C = native()
+            sums = C.bn_act_bwd_reduce(dz, z, y, mean, relu)     # [sum g, sum g*(y-mean)]
+            dbeta, dgamma = sums[0], sums[1] * invstd
+            dy, dres = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sums,
+                                          relu, training, has_res)
+            dx = C.conv_dgrad(dy, weight, list(x.shape), stride, pad) if need_x else None
+            dw = C.conv_wgrad(dy, x, list(weight.shape), stride, pad) if need_w else None
+        else:
+            dy, dgamma, dbeta, dres = ref.bn_act_bwd(dz, z, y, mean, invstd, gamma, relu,
+                                                     training, has_res, x.dtype)
+            dx = ref.conv2d_nhwc_dgrad(dy, weight, x.shape, stride, pad).to(x.dtype) if need_x else None
+            dw = ref.conv2d_nhwc_wgrad(dy, x, weight.shape, stride, pad) if need_w else None
+            if dw is not None:
+                dw = dw.contiguous(memory_format=torch.channels_last) \
+                    if weight.is_contiguous(memory_format=torch.channels_last) else dw
+        if dw is not None:
+            dw = dw.to(weight.dtype)
+        return (dx, dw, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), dres,
+                None, None, None, None, None, None, None, None)
+
+
+def conv_bn(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool,
+            residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """z = act(BN(conv(x)) [+ residual]) on NHWC activations."""
+    stride = conv.stride[0]
+    pad = conv.padding[0]
+    training = bn.training or not bn.track_running_stats
+    momentum = bn.momentum
+    if training and bn.track_running_stats:
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+        if momentum is None:  # cumulative moving average (torch BN semantics)
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    return _ConvBN.apply(x, conv.weight, bn.weight, bn.bias, residual,
+                         bn.running_mean, bn.running_var, stride, pad, relu,
+                         training, momentum if momentum is not None else 0.0, bn.eps)
+
+
+# ----------------------------------------------------------------------------
+# max pool 3x3/s2/p1
+# ----------------------------------------------------------------------------
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        if x.is_cuda:
+            y, idx = native().maxpool_fwd(x)       # idx: argmax position 0..8 per output (uint8)
+            ctx.save_for_backward(idx)
+        else:
+            y = ref.maxpool3x3s2_fwd(x)
+            ctx.save_for_backward(x)
+        ctx.hw = (x.shape[1], x.shape[2])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (saved,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        if dy.is_cuda:
+            return native().maxpool_bwd(dy, saved, ctx.hw[0], ctx.hw[1])
+        return ref.maxpool3x3s2_bwd(dy, saved)
+
+
+def maxpool3x3s2(x: torch.Tensor) -> torch.Tensor:
+    return _MaxPool.apply(x)
+
+
+# ----------------------------------------------------------------------------
+# global avg pool + fc
+# ----------------------------------------------------------------------------
+class _AvgPoolLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        if x.is_cuda:
+            pooled = native().avgpool_fwd(x)           # fp32 [N, C]
+        else:
+            pooled = ref.global_avgpool(x)
+        logits = torch.addmm(bias.float(), pooled, weight.float().t())
+        ctx.save_for_backward(pooled, weight)
+        ctx.hw = (x.shape[1], x.shape[2], x.dtype)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        pooled, weight = ctx.saved_tensors
+        h, w, dt = ctx.hw
+        dlogits = dlogits.float().contiguous()
+        dw = dlogits.t().mm(pooled)
+        db = dlogits.sum(0)
+        dpooled = dlogits.mm(weight.float())
+        if dlogits.is_cuda:
+            dx = native().avgpool_bwd(dpooled, h, w)
+        else:
+            dx = (dpooled / (h * w))[:, None, None, :].expand(-1, h, w, -1).to(dt).contiguous()
+        return dx, dw.to(weight.dtype), db.to(weight.dtype)
+
+
+def avgpool_linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    return _AvgPoolLinear.apply(x, weight, bias)
+
+
+# ----------------------------------------------------------------------------
+# softmax cross entropy (mean) -- fused fwd+bwd
+# ----------------------------------------------------------------------------
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        if logits.is_cuda:
+            loss, dlogits = native().softmax_xent(logits.contiguous(), labels.contiguous())
+        else:
+            loss, dlogits = ref.softmax_xent(logits, labels)
+        ctx.save_for_backward(dlogits)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dlogits,) = ctx.saved_tensors
+        return dlogits * dloss, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    return _SoftmaxXent.apply(logits, labels)
+
+
+class CrossEntropyLoss(nn.Module):
+    """Drop-in for ``nn.CrossEntropyLoss()`` (mean reduction, ``resnet/main.py:102``)."""
+
+    def forward(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        return cross_entropy(logits, labels)
+
+
+def top1_correct(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Number of rows whose argmax equals the label (``resnet/main.py:32-34``)."""
+    if logits.is_cuda:
+        return native().top1_correct(logits.contiguous(), labels.contiguous())
+    return ref.top1_correct(logits, labels)

@@ -1,0 +1,169 @@
+"""Trainer: the reference ``resnet/main.py`` behaviour on the MI355X framework.
+
+    torchrun --nproc_per_node=8 -m pytorch_distributed_tutorials_amd.train [flags]
+    python -m pytorch_distributed_tutorials_amd.launch --nproc_per_node=8 [flags]
+
+Flags and defaults follow the reference (``resnet/main.py:42-59``),
+with its defects fixed: ``--local_rank`` and ``--local-rank`` and the
+``LOCAL_RANK`` env var are all accepted (D5), ``--learning_rate`` is a float (D4),
+the default checkpoint name exists (D2), the sampler is re-seeded every epoch
+(D6), evaluation uses no augmentation (D7), the device is bound before the
+process group comes up (D9), resume also restores optimizer state and epoch
+through a sidecar file (D10), and the process group is torn down at exit (D12).
+
+Behaviour kept: per-process batch 256, SGD(momentum 0.9, wd 1e-5),
+CrossEntropyLoss(mean), DistributedSampler sharding, rank-0 evaluation +
+checkpoint every 10 epochs *before* training that epoch, test batch 128, the
+stdout lines of ``resnet/main.py:107,113-115``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .data import DeviceLoader, DistributedSampler, build_dataset
+from .models import build_model
+from .optim import SGD
+from .parallel import DistributedDataParallel, destroy, init_distributed
+from .utils.checkpoint import load_checkpoint, save_checkpoint
+from .utils.seed import set_random_seeds
+
+DEFAULTS = {
+    "num_epochs": 10000,
+    "batch_size": 256,
+    "lr": 0.01,
+    "seed": 0,
+    "model_dir": "saved_models",
+    "model_filename": "resnet_distributed.pth",
+}
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    p.add_argument("--local_rank", "--local-rank", dest="local_rank", type=int, default=None,
+                   help="Local rank (torch.distributed.launch); falls back to $LOCAL_RANK")
+    p.add_argument("--num_epochs", type=int, default=DEFAULTS["num_epochs"], help="Number of training epochs")
+    p.add_argument("--batch-size", "--batch_size", dest="batch_size", type=int,
+                   default=DEFAULTS["batch_size"], help="Training batch size (per process)")
+    p.add_argument("--learning_rate", "--learning-rate", dest="learning_rate", type=float,
+                   default=DEFAULTS["lr"], help="Learning rate")
+    p.add_argument("--seed", type=int, default=DEFAULTS["seed"], help="Random seed for training")
+    p.add_argument("--model_dir", type=str, default=DEFAULTS["model_dir"],
+                   help="Model directory to store saved models")
+    p.add_argument("--model_filename", type=str, default=DEFAULTS["model_filename"],
+                   help="Model filename to be saved")
+    p.add_argument("--resume", action="store_true", help="Resume training from saved checkpoint.")
+    # ---- framework extensions
+    p.add_argument("--arch", default="resnet18", choices=["resnet18", "resnet34", "resnet50",
+                                                          "resnet101", "resnet152"])
+    p.add_argument("--num-classes", type=int, default=1000,
+                   help="fc outputs (the reference keeps torchvision's 1000)")
+    p.add_argument("--impl", default="auto", choices=["auto", "native", "torch"],
+                   help="native = MI355X HIP kernels (GPU); torch = stock ATen ops")
+    p.add_argument("--data", default="cifar10",
+                   choices=["cifar10", "synthetic-cifar", "synthetic-imagenet"])
+    p.add_argument("--data-root", default="data")
+    p.add_argument("--synthetic-samples", type=int, default=None)
+    p.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])
+    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--eval-every", type=int, default=10)
+    p.add_argument("--max-steps-per-epoch", type=int, default=None)
+    p.add_argument("--timeout", type=float, default=None, help="collective timeout (s)")
+    p.add_argument("--log-every", type=int, default=0, help="print img/s every N steps (0 = off)")
+    return p
+
+
+def evaluate(model: nn.Module, device: torch.device, test_loader) -> float:
+    """Top-1 accuracy (``resnet/main.py:23-37``), fused argmax/compare/count on GPU."""
+    model.eval()
+    correct = torch.zeros((), dtype=torch.long, device=device)
+    total = 0
+    with torch.no_grad():
+        for images, labels in test_loader:
+            images, labels = images.to(device), labels.to(device)
+            outputs = model(images)
+            correct += ops.top1_correct(outputs, labels)
+            total += labels.size(0)
+    return correct.item() / max(total, 1)
+
+
+def main(argv: Optional[list] = None) -> int:
+    args = build_parser().parse_args(argv)
+    set_random_seeds(args.seed)
+    env = init_distributed(args.backend, args.local_rank, args.timeout)
+    local_rank = env.local_rank
+    use_cuda = torch.cuda.is_available() and args.backend != "gloo"
+    device = torch.device(f"cuda:{local_rank}") if use_cuda else torch.device("cpu")
+    impl = args.impl
+    if impl == "auto":
+        impl = "native" if device.type == "cuda" else "torch"
+
+    model = build_model(args.arch, num_classes=args.num_classes, impl=impl).to(device)
+    if impl == "native":
+        model.set_impl("native")  # re-assert channels_last weights after .to()
+    ddp_model = DistributedDataParallel(model, device_ids=[local_rank] if use_cuda else None,
+                                        output_device=local_rank if use_cuda else None,
+                                        bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
+    criterion = ops.CrossEntropyLoss() if impl == "native" else nn.CrossEntropyLoss()
+    optimizer = SGD(ddp_model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
+
+    model_filepath = os.path.join(args.model_dir, args.model_filename)
+    start_epoch = 0
+    if args.resume:
+        ep = load_checkpoint(ddp_model, model_filepath, device, optimizer)
+        if ep is not None:
+            start_epoch = int(ep)
+
+    n_train = args.synthetic_samples
+    train_set = build_dataset(args.data, True, args.data_root, n_train,
+                              num_classes=min(args.num_classes, 10 if "cifar" in args.data else 1000),
+                              seed=args.seed)
+    test_set = build_dataset(args.data, False, args.data_root,
+                             None if n_train is None else max(n_train // 5, 1),
+                             num_classes=min(args.num_classes, 10 if "cifar" in args.data else 1000),
+                             seed=args.seed)
+    train_sampler = DistributedSampler(len(train_set), num_replicas=env.world_size, rank=env.rank)
+    train_loader = DeviceLoader(train_set, args.batch_size, sampler=train_sampler, augment=True,
+                                device=device, seed=args.seed + env.rank)
+    test_loader = DeviceLoader(test_set, 128, shuffle=False, augment=False, device=device)
+
+    for epoch in range(start_epoch, args.num_epochs):
+        print("Local Rank: {}, Epoch: {}, Training ...".format(local_rank, epoch), flush=True)
+        if epoch % args.eval_every == 0 and local_rank == 0:
+            accuracy = evaluate(model=ddp_model, device=device, test_loader=test_loader)
+            save_checkpoint(ddp_model, model_filepath, optimizer, epoch)
+            print("-" * 75)
+            print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
+            print("-" * 75, flush=True)
+
+        ddp_model.train()
+        train_loader.set_epoch(epoch)
+        t0 = time.perf_counter()
+        for step, (inputs, labels) in enumerate(train_loader):
+            if args.max_steps_per_epoch is not None and step >= args.max_steps_per_epoch:
+                break
+            inputs, labels = inputs.to(device), labels.to(device)
+            optimizer.zero_grad()
+            outputs = ddp_model(inputs)
+            loss = criterion(outputs, labels)
+            loss.backward()
+            optimizer.step()
+            if args.log_every and (step + 1) % args.log_every == 0 and env.rank == 0:
+                if device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                print(f"  step {step + 1} loss {loss.item():.4f} "
+                      f"{(step + 1) * args.batch_size * env.world_size / dt:.1f} img/s", flush=True)
+    destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

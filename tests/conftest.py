@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X GPU (runs the HIP kernels)")
+    config.addinivalue_line("markers", "slow: multi-process / longer tests")
+
+
+@pytest.fixture(scope="session")
+def native_ext():
+    """Build (incrementally) and import the native extension; CPU-safe."""
+    import build_native
+    build_native.ensure_built()
+    from pytorch_distributed_tutorials_amd.ops import _ext
+    return _ext.native()
+
+
+@pytest.fixture(scope="session")
+def gpu(native_ext):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")

@@ -1,0 +1,256 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first so the reference sees exactly the kernel's
+operands; tolerances cover the fp32-accumulate vs fp32-reference ordering and the
+final bf16 rounding of outputs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_tutorials_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_SHAPES = [
+    # N, H, W, C, K, R, S, stride, pad
+    (2, 8, 8, 64, 64, 3, 3, 1, 1),
+    (2, 8, 8, 64, 128, 1, 1, 2, 0),
+    (2, 9, 9, 128, 128, 3, 3, 2, 1),
+    (3, 7, 7, 256, 512, 1, 1, 1, 0),
+    (4, 56, 56, 64, 256, 1, 1, 1, 0),     # 128x128 tile config
+    (8, 32, 32, 64, 64, 3, 3, 1, 1),      # 256x64 tile config
+    (2, 14, 14, 256, 256, 3, 3, 1, 1),
+    (2, 15, 15, 128, 256, 3, 3, 2, 1),
+    (2, 16, 16, 512, 64, 1, 1, 1, 0),
+]
+
+
+def _make(shape, dev, seed=0):
+    n, h, w, c, k, r, s, st, pd = shape
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    wt = (torch.randn(k, c, r, s, generator=g) / (c * r * s) ** 0.5).to(dev)
+    wt = wt.to(torch.bfloat16).float().contiguous(memory_format=torch.channels_last)
+    return x, wt
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_and_stats(gpu, native_ext, shape):
+    C = native_ext
+    x, w = _make(shape, gpu)
+    st, pd = shape[7], shape[8]
+    wk = C.pack_weight(w, x.shape[3])
+    y, part = C.conv_fwd(x, wk, st, pd, True)
+    yr = ref.conv2d_nhwc(x, w, st, pd)
+    assert y.shape == yr.shape
+    assert _rel_err(y, yr) < 1e-2
+    # BN finalize from the epilogue partials
+    k = w.shape[0]
+    m = yr.numel() // k
+    rm = torch.zeros(k, device=gpu)
+    rv = torch.ones(k, device=gpu)
+    gamma = torch.rand(k, device=gpu) + 0.5
+    beta = torch.randn(k, device=gpu)
+    stats = C.bn_finalize(part, m, rm, rv, gamma, beta, 0.1, 1e-5)
+    mean_r, var_r = ref.bn_batch_stats(yr)
+    assert torch.allclose(stats[0], mean_r, atol=2e-3, rtol=1e-2)
+    invstd_r = torch.rsqrt(var_r + 1e-5)
+    assert torch.allclose(stats[1], invstd_r, rtol=2e-2)
+    assert torch.allclose(rm, 0.1 * mean_r, atol=1e-3, rtol=1e-2)
+    assert torch.allclose(rv, 0.9 + 0.1 * var_r * m / (m - 1), rtol=1e-2)
+
+
+def test_conv_fwd_stem(gpu, native_ext):
+    C = native_ext
+    g = torch.Generator().manual_seed(1)
+    img = torch.randn(2, 3, 32, 32, generator=g).to(gpu)
+    x = C.image_to_nhwc(img)
+    assert x.shape == (2, 32, 32, 8)
+    assert torch.equal(x[..., :3].float(), img.permute(0, 2, 3, 1).to(torch.bfloat16).float())
+    assert x[..., 3:].abs().max().item() == 0
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu).to(torch.bfloat16).float()
+    w = w.contiguous(memory_format=torch.channels_last)
+    wk = C.pack_weight(w, 8)
+    y, _ = C.conv_fwd(x, wk, 2, 3, False)
+    yr = ref.conv2d_nhwc(x, w, 2, 3)
+    assert _rel_err(y, yr) < 1e-2
+    # wgrad of the stem (C padded to 8 internally, sliced back to 3)
+    dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16).to(gpu)
+    dw = C.conv_wgrad(dy, x, list(w.shape), 2, 3)
+    dwr = ref.conv2d_nhwc_wgrad(dy, x, w.shape, 2, 3)
+    assert dw.shape == dwr.shape
+    assert _rel_err(dw, dwr) < 1e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_dgrad(gpu, native_ext, shape):
+    C = native_ext
+    x, w = _make(shape, gpu, seed=3)
+    st, pd = shape[7], shape[8]
+    yr = ref.conv2d_nhwc(x, w, st, pd)
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16).to(gpu)
+    dx = C.conv_dgrad(dy, w, list(x.shape), st, pd)
+    dxr = ref.conv2d_nhwc_dgrad(dy, w, x.shape, st, pd)
+    assert dx.shape == dxr.shape
+    assert _rel_err(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_wgrad(gpu, native_ext, shape):
+    C = native_ext
+    x, w = _make(shape, gpu, seed=7)
+    st, pd = shape[7], shape[8]
+    yr = ref.conv2d_nhwc(x, w, st, pd)
+    g = torch.Generator().manual_seed(9)
+    dy = torch.randn(yr.shape, generator=g).to(torch.bfloat16).to(gpu)
+    dw = C.conv_wgrad(dy, x, list(w.shape), st, pd)
+    dwr = ref.conv2d_nhwc_wgrad(dy, x, w.shape, st, pd)
+    assert dw.shape == dwr.shape
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    assert _rel_err(dw, dwr) < 1e-2
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_act_fwd_bwd(gpu, native_ext, relu, res):
+    C = native_ext
+    g = torch.Generator().manual_seed(11)
+    n, h, w, k = 4, 7, 9, 128
+    y = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
+    r = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu) if res else None
+    gamma = (torch.rand(k, generator=g) + 0.5).to(gpu)
+    beta = torch.randn(k, generator=g).to(gpu)
+    mean, var = ref.bn_batch_stats(y)
+    invstd = torch.rsqrt(var + 1e-5)
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    z = C.bn_act_fwd(y, scale, shift, r, relu)
+    zr = ref.bn_act_fwd(y, mean, invstd, gamma, beta, r, relu, torch.float32)
+    assert (z.float() - zr).abs().max().item() < 3e-2
+    dz = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
+    sums = C.bn_act_bwd_reduce(dz, z, y, mean, relu)
+    dy, dres = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sums, relu, True, res)
+    dyr, dgr, dbr, dresr = ref.bn_act_bwd(dz, z, y, mean, invstd, gamma, relu, True, res, torch.float32)
+    assert torch.allclose(sums[0], dbr, rtol=1e-3, atol=1e-2)
+    assert torch.allclose(sums[1] * invstd, dgr, rtol=1e-3, atol=1e-2)
+    assert _rel_err(dy, dyr) < 1e-2
+    if res:
+        assert _rel_err(dres, dresr) < 1e-2
+
+
+def test_bn_against_torch_batchnorm(gpu, native_ext):
+    """Full BN fwd/bwd semantics vs torch.nn.functional.batch_norm (training)."""
+    C = native_ext
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(8, 64, 6, 6, generator=g).to(gpu)
+    xb = x.to(torch.bfloat16).float().requires_grad_(True)
+    gamma = (torch.rand(64, generator=g) + 0.5).to(gpu).requires_grad_(True)
+    beta = torch.randn(64, generator=g).to(gpu).requires_grad_(True)
+    out = F.relu(F.batch_norm(xb, None, None, gamma, beta, training=True, eps=1e-5))
+    gout = torch.randn(out.shape, generator=g).to(gpu)
+    out.backward(gout)
+    y = xb.detach().permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    mean, var = ref.bn_batch_stats(y)
+    invstd = torch.rsqrt(var + 1e-5)
+    z = C.bn_act_fwd(y, gamma.detach() * invstd, beta.detach() - mean * gamma.detach() * invstd, None, True)
+    assert _rel_err(z.permute(0, 3, 1, 2), out) < 1e-2
+    dz = gout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    sums = C.bn_act_bwd_reduce(dz, z, y, mean, True)
+    dy, _ = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma.detach(), sums, True, True, False)
+    assert _rel_err(dy.permute(0, 3, 1, 2), xb.grad) < 3e-2
+    assert _rel_err(sums[1] * invstd, gamma.grad) < 3e-2
+    assert _rel_err(sums[0], beta.grad) < 3e-2
+
+
+def test_maxpool(gpu, native_ext):
+    C = native_ext
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(2, 17, 16, 64, generator=g)
+    x = torch.relu(x).to(torch.bfloat16).to(gpu)  # many exact zeros -> exercises tie-breaking
+    y, idx = C.maxpool_fwd(x)
+    yr = ref.maxpool3x3s2_fwd(x)
+    assert torch.equal(y, yr)
+    dy = torch.randn(y.shape, generator=g).to(torch.bfloat16).to(gpu)
+    dx = C.maxpool_bwd(dy, idx, x.shape[1], x.shape[2])
+    dxr = ref.maxpool3x3s2_bwd(dy, x)
+    assert (dx.float() - dxr.float()).abs().max().item() < 2e-2
+
+
+def test_avgpool(gpu, native_ext):
+    C = native_ext
+    x = torch.randn(4, 7, 7, 2048, device=gpu).to(torch.bfloat16)
+    y = C.avgpool_fwd(x)
+    assert torch.allclose(y, x.float().mean((1, 2)), atol=1e-3)
+    dy = torch.randn(4, 2048, device=gpu)
+    dx = C.avgpool_bwd(dy, 7, 7)
+    assert torch.allclose(dx.float(), (dy / 49)[:, None, None, :].expand(4, 7, 7, 2048), atol=1e-3, rtol=1e-2)
+
+
+def test_softmax_xent_and_top1(gpu, native_ext):
+    C = native_ext
+    g = torch.Generator().manual_seed(17)
+    logits = (torch.randn(64, 1000, generator=g) * 3).to(gpu)
+    labels = torch.randint(0, 1000, (64,), generator=g).to(gpu)
+    loss, dl = C.softmax_xent(logits, labels)
+    lr_, dlr = ref.softmax_xent(logits, labels)
+    assert abs(loss.item() - lr_.item()) < 1e-4
+    assert torch.allclose(dl, dlr, atol=1e-6)
+    labels[:10] = logits[:10].argmax(1)
+    cnt = C.top1_correct(logits, labels)
+    assert cnt.item() == (logits.argmax(1) == labels).sum().item()
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_sgd_flat(gpu, native_ext, nesterov):
+    C = native_ext
+    n = 10001
+    p = torch.randn(n, device=gpu)
+    gr = torch.randn(n, device=gpu)
+    buf = torch.empty(n, device=gpu)
+    p2, b2 = p.clone(), torch.empty(n, device=gpu)
+    for first in (True, False):
+        C.sgd_step(p, gr, buf, 0.1, 0.9, 0.0, 1e-4, nesterov, first, 1.0)
+        ref.sgd_momentum_([p2], [gr], [b2], 0.1, 0.9, 0.0, 1e-4, nesterov, first)
+    assert torch.allclose(p, p2, atol=1e-6)
+    assert torch.allclose(buf, b2, atol=1e-6)
+
+
+def test_rccl_comm_single_rank(gpu, native_ext):
+    C = native_ext
+    comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1, 0)
+    t = torch.arange(1024, dtype=torch.float32, device=gpu)
+    comm.all_reduce(t, "avg")
+    comm.broadcast(t, 0)
+    comm.current_wait_comm()
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.arange(1024, dtype=torch.float32, device=gpu))
+
+
+def test_resnet18_native_matches_torch(gpu, native_ext):
+    """Native NHWC bf16 model vs the stock fp32 torch model with identical weights."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    torch.manual_seed(0)
+    mt = build_model("resnet18", num_classes=10)
+    mn = copy.deepcopy(mt).to(gpu).set_impl("native")
+    x = torch.randn(16, 3, 32, 32)
+    y = torch.randint(0, 10, (16,))
+    lt = F.cross_entropy(mt(x), y)
+    lt.backward()
+    ln = ops.cross_entropy(mn(x.to(gpu)), y.to(gpu))
+    ln.backward()
+    assert abs(ln.item() - lt.item()) < 5e-2 * max(1.0, abs(lt.item()))
+    for (name, pt), (_, pn) in zip(mt.named_parameters(), mn.named_parameters()):
+        a, b = pn.grad.float().cpu().flatten(), pt.grad.flatten()
+        cos = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
+        assert cos > 0.97, f"{name}: cosine {cos}"
+    for (name, bt), (_, bn) in zip(mt.named_buffers(), mn.named_buffers()):
+        assert torch.allclose(bn.float().cpu(), bt.float(), atol=5e-2, rtol=5e-2), name
