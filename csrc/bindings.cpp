@@ -124,7 +124,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
 
 // dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
-                  int64_t pad) {
+                  int64_t pad, bool deterministic) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(x, "x");
   TORCH_CHECK(ws.size() == 4, "weight shape must be [K,C,R,S]");
@@ -135,10 +135,10 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && K == dy.size(3), "wgrad: dy shape mismatch");
   auto fopt = x.options().dtype(at::kFloat);
   auto dwp = at::empty({K, R, S, Cx}, fopt);
-  size_t wsn = pdt::conv_wgrad_ws_floats(s);
+  size_t wsn = pdt::conv_wgrad_ws_floats(s, deterministic);
   Tensor wsb = wsn ? at::empty({(int64_t)wsn}, fopt) : Tensor();
   pdt::launch_conv_wgrad(cbf(dy), cbf(x), dwp.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
-                         s, cur_stream(x));
+                         s, deterministic, cur_stream(x));
   Tensor krsc = Cx == C ? dwp : dwp.narrow(3, 0, C).contiguous();
   return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
 }
@@ -322,7 +322,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("stats"));
   m.def("conv_dgrad", &conv_dgrad);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
+        py::arg("pad"), py::arg("deterministic") = false);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_params", &bn_eval_params);
   m.def("bn_act_fwd", &bn_act_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"),

@@ -226,17 +226,29 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
   }
 }
 
+// block = 32 channels x 8 partial-lanes; each lane sums nb/8 stage-1 partials (independent
+// loads, pipelined), then an LDS combine.  Deterministic (fixed order).
 __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restrict__ ws, int nb,
                                                             int K, float* __restrict__ sums) {
-  int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
+  __shared__ float sa[8][33], sb[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int k = blockIdx.x * 32 + tx;
   float a = 0.f, b = 0.f;
-  for (int i = 0; i < nb; ++i) {
-    a += ws[(int64_t)i * 2 * K + k];
-    b += ws[(int64_t)i * 2 * K + K + k];
+  if (k < K) {
+#pragma unroll 4
+    for (int i = ty; i < nb; i += 8) {
+      a += ws[(int64_t)i * 2 * K + k];
+      b += ws[(int64_t)i * 2 * K + K + k];
+    }
   }
-  sums[k] = a;       // sum g          (= dbeta)
-  sums[K + k] = b;   // sum g*(y-mean) (dgamma = b*invstd)
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && k < K) {
+    for (int r = 1; r < 8; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
+    sums[k] = a;       // sum g          (= dbeta)
+    sums[K + k] = b;   // sum g*(y-mean) (dgamma = b*invstd)
+  }
 }
 
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
@@ -252,7 +264,7 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
     hipLaunchKernelGGL(bn_bwd_reduce_stage1<true>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, mean, M, K8, ws);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_stage1<false>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, mean, M, K8, ws);
-  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 256)), dim3(256), 0, st, ws, nb, K, sums);
+  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K, sums);
 }
 
 // ------------------------------------------------------------- backward apply

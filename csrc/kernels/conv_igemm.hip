@@ -381,7 +381,7 @@ struct TnCfg {
   static constexpr int TN = BNG / 2 / 16;
 };
 
-template <int BMG, int BNG, bool C64>
+template <int BMG, int BNG, bool ATOMIC>
 __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   using CFG = TnCfg<BMG, BNG>;
   constexpr int TM = CFG::TM, TN = CFG::TN;
@@ -513,9 +513,11 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
     __syncthreads();
   }
 
-  // epilogue: fp32 [Kout][Ncols] slab of this split; lane holds rows fq*4+e, column fr
+  // epilogue: lane holds rows fq*4+e, column fr.  ATOMIC: fp32 atomic add into the zeroed dW
+  // (16 lanes = 64 contiguous bytes per row; split count bounded so atomic bytes stay small);
+  // otherwise a private fp32 [Kout][Ncols] slab per split, summed by splitk_reduce_kernel.
   const int fq = lane >> 4, fr = lane & 15;
-  float* o = P.out + (int64_t)split * P.Kout * P.Ncols;
+  float* o = ATOMIC ? P.out : P.out + (int64_t)split * P.Kout * P.Ncols;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -525,7 +527,10 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         int row = k0 + wm * TM * 16 + i * 16 + fq * 4 + e;
-        if (row < P.Kout) o[(int64_t)row * P.Ncols + col] = acc[i][j][e];
+        if (row < P.Kout) {
+          if (ATOMIC) unsafeAtomicAdd(o + (int64_t)row * P.Ncols + col, acc[i][j][e]);
+          else o[(int64_t)row * P.Ncols + col] = acc[i][j][e];
+        }
       }
     }
 }
@@ -668,7 +673,7 @@ struct WgradPlan {
   int bmg, bng, tiles, splits, steps_per_split, nsteps;
 };
 
-static WgradPlan plan_wgrad(const ConvShape& s) {
+static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   WgradPlan p;
   p.bmg = s.K <= 64 ? 64 : 128;
   p.bng = 128;
@@ -679,22 +684,27 @@ static WgradPlan plan_wgrad(const ConvShape& s) {
   int target = 1024;  // ~4 blocks per CU
   int splits = (target + p.tiles - 1) / p.tiles;
   splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
+  // bound the reduction traffic: atomics/slabs move splits * |dW| * 4 bytes
+  const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
+  const int64_t cap_bytes = deterministic ? ((int64_t)64 << 20) : ((int64_t)32 << 20);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, cap_bytes / dw_bytes));
   splits = std::max(1, std::min(splits, 256));
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   return p;
 }
 
-size_t conv_wgrad_ws_floats(const ConvShape& s) {
-  WgradPlan p = plan_wgrad(s);
+size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
+  if (!deterministic) return 0;
+  WgradPlan p = plan_wgrad(s, true);
   if (p.splits <= 1) return 0;
   return (size_t)p.splits * s.K * s.R * s.S * s.C;
 }
 
-template <int BMG, int BNG>
+template <int BMG, int BNG, bool ATOMIC>
 static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
   using CFG = TnCfg<BMG, BNG>;
-  auto kfn = igemm_tn_kernel<BMG, BNG, true>;
+  auto kfn = igemm_tn_kernel<BMG, BNG, ATOMIC>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -705,12 +715,14 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
 }
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, hipStream_t st) {
+                       const ConvShape& s, bool deterministic, hipStream_t st) {
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
-  WgradPlan p = plan_wgrad(s);
+  WgradPlan p = plan_wgrad(s, deterministic);
+  const bool slab = deterministic && p.splits > 1;
+  const bool atomic = !deterministic && p.splits > 1;
   TnArgs a{};
   a.dy = dy; a.x = x;
-  a.out = p.splits > 1 ? ws : dw;
+  a.out = slab ? ws : dw;
   a.dy_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
   a.x_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
   a.Mred = s.N * s.Ho * s.Wo; a.Kout = s.K; a.Ncols = s.R * s.S * s.C;
@@ -720,10 +732,16 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.div_w = make_fastdiv((uint32_t)s.Wo);
   a.steps_per_split = p.steps_per_split;
   a.nsteps = p.nsteps;
-  if (p.bmg == 64) run_tn<64, 128>(a, p.tiles, p.splits, st);
-  else run_tn<128, 128>(a, p.tiles, p.splits, st);
-  if (p.splits > 1) {
-    int64_t n = (int64_t)s.K * a.Ncols;
+  const int64_t n = (int64_t)s.K * a.Ncols;
+  if (atomic) hipMemsetAsync(dw, 0, n * sizeof(float), st);
+  if (p.bmg == 64) {
+    if (atomic) run_tn<64, 128, true>(a, p.tiles, p.splits, st);
+    else run_tn<64, 128, false>(a, p.tiles, p.splits, st);
+  } else {
+    if (atomic) run_tn<128, 128, true>(a, p.tiles, p.splits, st);
+    else run_tn<128, 128, false>(a, p.tiles, p.splits, st);
+  }
+  if (slab) {
     int64_t b = (n / 4 + 255) / 256;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 4096))),
                        dim3(256), 0, st, ws, p.splits, n, dw);

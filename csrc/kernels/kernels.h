@@ -33,10 +33,11 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (all stride/pad combos, parity classes)
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvShape& s,
                        hipStream_t st);
-// dw[K][R][S][C] (fp32) = wgrad(dy, x).  ws: fp32 workspace of conv_wgrad_ws_floats() floats.
-size_t conv_wgrad_ws_floats(const ConvShape& s);
+// dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
+// (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
+size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, hipStream_t st);
+                       const ConvShape& s, bool deterministic, hipStream_t st);
 
 // -------------------------------------------------------------- bn_act.hip
 // part[ngroups][2][K] (group g has min(grows, M-grows*g) rows) -> out[4][K] = mean, invstd,

@@ -34,8 +34,25 @@ def parse(argv):
     p.add_argument("--no-python", action="store_true", help="run the first positional as an executable")
     p.add_argument("--use-local-rank-arg", action="store_true",
                    help="also pass --local-rank=N (torch.distributed.launch style)")
-    p.add_argument("rest", nargs=argparse.REMAINDER)
-    return p.parse_args(argv)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    # launcher options come first; everything from the first unknown token on belongs to
+    # the per-rank program (like torchrun: options, then script/module, then its args)
+    valued = {"--nproc_per_node", "--nproc-per-node", "--master_addr", "--master-addr",
+              "--master_port", "--master-port"}
+    flags = {"-m", "--module", "--no-python", "--use-local-rank-arg", "-h", "--help"}
+    i = 0
+    while i < len(argv):
+        tok = argv[i]
+        name = tok.split("=", 1)[0]
+        if name in valued:
+            i += 1 if "=" in tok else 2
+        elif tok in flags:
+            i += 1
+        else:
+            break
+    a = p.parse_args(argv[:i])
+    a.rest = argv[i:]
+    return a
 
 
 DEFAULT_MODULE = "pytorch_distributed_tutorials_amd.train"

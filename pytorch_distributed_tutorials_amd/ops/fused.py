@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import reference as ref
+from ..utils.seed import deterministic
 from ._ext import native
 
 _CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
@@ -100,7 +101,8 @@ class _ConvBN(torch.autograd.Function):
             dy, dres = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sums,
                                           relu, training, has_res)
             dx = C.conv_dgrad(dy, weight, list(x.shape), stride, pad) if need_x else None
-            dw = C.conv_wgrad(dy, x, list(weight.shape), stride, pad) if need_w else None
+            dw = C.conv_wgrad(dy, x, list(weight.shape), stride, pad, deterministic()) \
+                if need_w else None
         else:
             dy, dgamma, dbeta, dres = ref.bn_act_bwd(dz, z, y, mean, invstd, gamma, relu,
                                                      training, has_res, x.dtype)

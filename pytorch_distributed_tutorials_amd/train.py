@@ -77,6 +77,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-steps-per-epoch", type=int, default=None)
     p.add_argument("--timeout", type=float, default=None, help="collective timeout (s)")
     p.add_argument("--log-every", type=int, default=0, help="print img/s every N steps (0 = off)")
+    p.add_argument("--deterministic", action=argparse.BooleanOptionalAction, default=True,
+                   help="bitwise-reproducible kernels (reference sets cudnn.deterministic=True); "
+                        "--no-deterministic enables atomic split-K weight gradients")
     return p
 
 
@@ -96,7 +99,7 @@ def evaluate(model: nn.Module, device: torch.device, test_loader) -> float:
 
 def main(argv: Optional[list] = None) -> int:
     args = build_parser().parse_args(argv)
-    set_random_seeds(args.seed)
+    set_random_seeds(args.seed, deterministic=args.deterministic)
     env = init_distributed(args.backend, args.local_rank, args.timeout)
     local_rank = env.local_rank
     use_cuda = torch.cuda.is_available() and args.backend != "gloo"
