@@ -109,7 +109,7 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& wk, int64_t s
 }
 
 Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, int64_t stride,
-                  int64_t pad) {
+                  int64_t pad, const std::optional<Tensor>& addend) {
   check_bf16_nhwc(dy, "dy");
   TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
   TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
@@ -118,7 +118,13 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
   Tensor wt = pack_weight_t(w);
   auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
-  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), s, cur_stream(dy));
+  const uint16_t* ap = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16_nhwc(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    ap = cbf(*addend);
+  }
+  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, cur_stream(dy));
   return dx;
 }
 
@@ -321,7 +327,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_weight_t", &pack_weight_t);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("stats"));
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"), py::arg("stride"),
+        py::arg("pad"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false);
   m.def("bn_finalize", &bn_finalize);

@@ -85,6 +85,7 @@ struct NtArgs {
   const uint16_t* a;   // activation source NHWC (x for fwd, dy for dgrad), CA channels
   const uint16_t* b;   // [Nout][Kg] k-contiguous
   uint16_t* out;       // NHWC output, Nout channels
+  const uint16_t* addend;  // optional NHWC tensor (same layout as out) added in the epilogue
   float* part;         // BN partials [ngroups][2][Nout] or null
   uint32_t a_bytes, b_bytes;
   int HA, WA, CA;      // A source dims
@@ -94,6 +95,7 @@ struct NtArgs {
   int Mij, Mj;
   int ash, asw, aoff_h, aoff_w;     // A base coords: h0 = i*ash + aoff_h
   int OH, OW, osh, osw, oph, opw;   // out row = (n*OH + i*osh + oph)*OW + j*osw + opw
+  int dense;           // output row == m (no scatter)
   int ntaps;
   int8_t tdr[MAX_TAPS], tds[MAX_TAPS];
   int16_t tb[MAX_TAPS];
@@ -109,21 +111,37 @@ __device__ __forceinline__ int swz128(int row, int chunk) {
 template <int WM, int WN, int TM, int TN>
 struct NtCfg {
   static constexpr int NT = WM * WN * 64;
+  static constexpr int WAVES = WM * WN;
   static constexpr int BM = WM * TM * 16;
   static constexpr int BN = WN * TN * 16;
-  static constexpr int A_PT = BM * 8 / NT;  // 16-B chunks per thread (8 chunks per 64-wide row)
-  static constexpr int B_PT = BN * 8 / NT;
-  static constexpr int ROWSTEP = NT / 8;
+  // one LDS-DMA wave instruction moves 64 lanes x 16 B = 8 rows of a [rows][64] bf16 tile
+  static constexpr int A_PW = BM / 8 / WAVES;  // instructions per wave per K-step
+  static constexpr int B_PW = BN / 8 / WAVES;
+  static_assert(A_PW * 8 * WAVES == BM && B_PW * 8 * WAVES == BN, "tile rows must split over waves");
   static constexpr int PIPE_BYTES = 2 * (BM + BN) * 128;
-  static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row
-  static constexpr int EPI_BYTES = WM * WN * (TM * 16) * EPI_PITCH;
+  static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row (pixel)
+  static constexpr int EPI_BYTES = WAVES * (TM * 16) * EPI_PITCH;
   static constexpr int SMEM = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
 };
 
+// 16-byte LDS-DMA: every lane fetches 16 B at its own buffer offset (out-of-range -> 0) and the
+// wave's 64 results land contiguously at `lds` (wave-uniform base, lane-linear image).
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)(reinterpret_cast<uintptr_t>(lds)), 16, voff, 0, 0, 0);
+}
+
+// Main loop: LDS-DMA staging (no VGPR round trip, no ds_write), the XOR swizzle applied on the
+// SOURCE side (lane slot j of row r fetches chunk j ^ f(r)) so the lane-linear LDS image equals
+// the swizzled image swz128() reads.  Two buffers: the DMA of tile k+1 is issued before the MFMAs
+// of tile k; one vmcnt(0)+barrier per K-step.
+// MFMA operands are swapped (A = weights, B = pixels) so each lane's 4 accumulator registers are
+// 4 consecutive output channels of one pixel: the epilogue packs them into one 8-byte LDS write
+// and the BN statistics reduce over the 16 pixel-lanes with DPP-friendly xor shuffles.
 template <int WM, int WN, int TM, int TN, bool C64, bool STATS>
 __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) {
   using CFG = NtCfg<WM, WN, TM, TN>;
-  constexpr int BM = CFG::BM, BN = CFG::BN;
+  constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Nout + BN - 1) / BN;
@@ -133,16 +151,19 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   const int m0 = tmi * BM, n0 = tni * BN;
 
   const int t = threadIdx.x;
-  const int cc = t & 7;
-  const int rbase = t >> 3;
+  const int lane = t & 63, wid = t >> 6;
+  const int lr = lane >> 3, lj = lane & 7;
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
 
-  int a_pix[CFG::A_PT], a_h0[CFG::A_PT], a_w0[CFG::A_PT];
+  // A rows (pixels) and B rows (output channels) this lane fetches, fixed over the K loop
+  int a_pix[A_PW], a_h0[A_PW], a_w0[A_PW], a_c[A_PW];
 #pragma unroll
-  for (int i = 0; i < CFG::A_PT; ++i) {
-    int m = m0 + rbase + CFG::ROWSTEP * i;
+  for (int i = 0; i < A_PW; ++i) {
+    const int row = (wid * A_PW + i) * 8 + lr;
+    a_c[i] = lj ^ ((row >> 1) & 7);
+    const int m = m0 + row;
     if (m < P.M) {
       uint32_t n = fdiv((uint32_t)m, P.div_ij);
       uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
@@ -155,69 +176,60 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       a_pix[i] = 0; a_h0[i] = -(1 << 20); a_w0[i] = 0;
     }
   }
-  int b_row[CFG::B_PT];
+  int b_row[B_PW], b_c[B_PW];
 #pragma unroll
-  for (int i = 0; i < CFG::B_PT; ++i) {
-    int n = n0 + rbase + CFG::ROWSTEP * i;
+  for (int i = 0; i < B_PW; ++i) {
+    const int row = (wid * B_PW + i) * 8 + lr;
+    b_c[i] = lj ^ ((row >> 1) & 7);
+    const int n = n0 + row;
     b_row[i] = n < P.Nout ? n * P.Kg : -1;
   }
 
   const int cb = P.CA >> 6;
   const int nk = C64 ? P.ntaps * cb : (P.Kg + 63) / 64;
 
-  v4i ra_reg[CFG::A_PT], rb_reg[CFG::B_PT];
-
-  auto load_tiles = [&](int kt) {
+  auto issue = [&](int kt, int buf) {
+    char* As = smem + buf * (BM + BN) * 128;
+    char* Bs = As + BM * 128;
     if constexpr (C64) {
       const int tap = kt / cb;
-      const int ch = (kt - tap * cb) * 64 + cc * 8;
+      const int chb = (kt - tap * cb) * 64;
       const int dr = P.tdr[tap], ds = P.tds[tap];
-      const int tbo = (int)P.tb[tap] * P.CA + ch;
+      const int tbo = (int)P.tb[tap] * P.CA + chb;
 #pragma unroll
-      for (int i = 0; i < CFG::A_PT; ++i) {
+      for (int i = 0; i < A_PW; ++i) {
         int h = a_h0[i] + dr, w = a_w0[i] + ds;
         bool ok = (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
-        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * 2) : OOB;
-        ra_reg[i] = buf_load16(ra, off);
+        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + chb + a_c[i] * 8) * 2) : OOB;
+        glds16(ra, As + (wid * A_PW + i) * 1024, off);
       }
 #pragma unroll
-      for (int i = 0; i < CFG::B_PT; ++i) {
-        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * 2) : OOB;
-        rb_reg[i] = buf_load16(rb, off);
+      for (int i = 0; i < B_PW; ++i) {
+        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo + b_c[i] * 8) * 2) : OOB;
+        glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     } else {
-      const int kk = kt * 64 + cc * 8;
-      const bool kok = kk < P.Kg;
-      const int tap = kk / P.CA;
-      const int ch = kk - tap * P.CA;
-      const int r = tap / P.S;
-      const int s = tap - r * P.S;
 #pragma unroll
-      for (int i = 0; i < CFG::A_PT; ++i) {
+      for (int i = 0; i < A_PW; ++i) {
+        const int kk = kt * 64 + a_c[i] * 8;
+        const int tap = kk / P.CA;
+        const int ch = kk - tap * P.CA;
+        const int r = tap / P.S;
+        const int s = tap - r * P.S;
         int h = a_h0[i] + r, w = a_w0[i] + s;
-        bool ok = kok && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
+        bool ok = kk < P.Kg && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
         uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * 2) : OOB;
-        ra_reg[i] = buf_load16(ra, off);
+        glds16(ra, As + (wid * A_PW + i) * 1024, off);
       }
 #pragma unroll
-      for (int i = 0; i < CFG::B_PT; ++i) {
-        uint32_t off = (kok && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * 2) : OOB;
-        rb_reg[i] = buf_load16(rb, off);
+      for (int i = 0; i < B_PW; ++i) {
+        const int kk = kt * 64 + b_c[i] * 8;
+        uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * 2) : OOB;
+        glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     }
   };
-  auto store_tiles = [&](int buf) {
-    char* As = smem + buf * (BM + BN) * 128;
-    char* Bs = As + BM * 128;
-#pragma unroll
-    for (int i = 0; i < CFG::A_PT; ++i)
-      *reinterpret_cast<v4i*>(As + swz128(rbase + CFG::ROWSTEP * i, cc)) = ra_reg[i];
-#pragma unroll
-    for (int i = 0; i < CFG::B_PT; ++i)
-      *reinterpret_cast<v4i*>(Bs + swz128(rbase + CFG::ROWSTEP * i, cc)) = rb_reg[i];
-  };
 
-  const int wid = t >> 6, lane = t & 63;
   const int wm = wid % WM, wn = wid / WM;
   const int fr = lane & 15, fq = lane >> 4;
 
@@ -227,14 +239,12 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    load_tiles(0);
-    store_tiles(0);
-  }
+  if (nk > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(kt + 1);
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
     const char* As = smem + cur * (BM + BN) * 128;
     const char* Bs = As + BM * 128;
 #pragma unroll
@@ -242,95 +252,100 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       const int kc = ks * 4 + fq;
       v4i af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        int row = wm * TM * 16 + i * 16 + fr;
-        af[i] = *reinterpret_cast<const v4i*>(As + swz128(row, kc));
-      }
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const v4i*>(As + swz128(wm * TM * 16 + i * 16 + fr, kc));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int row = wn * TN * 16 + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(row, kc));
-      }
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(wn * TN * 16 + j * 16 + fr, kc));
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // --------------------------------------------------------------- epilogue
-  const int wrow0 = m0 + wm * TM * 16;  // first GEMM row of this wave
-  const int wcol0 = n0 + wn * TN * 16;
+  // lane (fq, fr), register e of acc[i][j]: pixel i*16 + fr, channel j*16 + fq*4 + e
+  const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
+  const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
 
   if constexpr (STATS) {
-    // per column: sum and M2 over this wave's TM*16 rows (valid rows only)
+    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels;
+    // the writer converts to M2 about the group mean (cancellation is benign at 64 rows; groups
+    // are combined with Chan's parallel formula in bn_finalize).
     const int group = tmi * WM + wm;
     const int valid = min(TM * 16, P.M - wrow0);
     if (valid > 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        float s = 0.f;
+        float s[4], q[4];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int e = 0; e < 4; ++e) {
+          float v = 0.f, v2 = 0.f;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            int r = i * 16 + fq * 4 + e;
-            s += r < valid ? acc[i][j][e] : 0.f;
+          for (int i = 0; i < TM; ++i) {
+            const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
+            v += a;
+            v2 = fmaf(a, a, v2);
           }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        const float mu = s / (float)valid;
-        float q = 0.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            int r = i * 16 + fq * 4 + e;
-            float d = acc[i][j][e] - mu;
-            q += r < valid ? d * d : 0.f;
+          for (int o = 1; o < 16; o <<= 1) {
+            v += __shfl_xor(v, o, 64);
+            v2 += __shfl_xor(v2, o, 64);
           }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        const int col = wcol0 + j * 16 + fr;
-        if (fq == 0 && col < P.Nout) {
-          P.part[((int64_t)group * 2 + 0) * P.Nout + col] = s;
-          P.part[((int64_t)group * 2 + 1) * P.Nout + col] = q;
+          s[e] = v;
+          q[e] = fmaxf(v2 - v * v / (float)valid, 0.f);
+        }
+        const int col = wcol0 + j * 16 + fq * 4;
+        if (fr == 0 && col < P.Nout) {
+          *reinterpret_cast<float4*>(P.part + ((int64_t)group * 2 + 0) * P.Nout + col) =
+              make_float4(s[0], s[1], s[2], s[3]);
+          *reinterpret_cast<float4*>(P.part + ((int64_t)group * 2 + 1) * P.Nout + col) =
+              make_float4(q[0], q[1], q[2], q[3]);
         }
       }
     }
   }
 
-  // stage the wave's TM*16 x TN*16 tile as bf16 in LDS, then store 16-B row chunks
+  // stage the wave's pixels x channels tile as bf16 (8-byte writes), then 16-byte row stores
   char* ep = smem + wid * (TM * 16) * CFG::EPI_PITCH;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int r = i * 16 + fq * 4 + e;
-        int c = j * 16 + fr;
-        *reinterpret_cast<uint16_t*>(ep + r * CFG::EPI_PITCH + c * 2) = f2bf(acc[i][j][e]);
-      }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private region, no barrier needed
+    for (int j = 0; j < TN; ++j) {
+      uint2 v;
+      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(ep + (i * 16 + fr) * CFG::EPI_PITCH + (j * 16 + fq * 4) * 2) = v;
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region is wave-private, no barrier needed
   __builtin_amdgcn_wave_barrier();
   constexpr int CH_PER_ROW = TN * 2;  // 16-B chunks per wave-tile row
   constexpr int CHUNKS = TM * 16 * CH_PER_ROW;
-#pragma unroll
-  for (int q = lane; q < CHUNKS; q += 64) {
-    int r = q / CH_PER_ROW, c = q - r * CH_PER_ROW;
+  for (int qd = lane; qd < CHUNKS; qd += 64) {
+    int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
     int m = wrow0 + r;
     int col = wcol0 + c * 8;
     if (m < P.M && col < P.Nout) {
-      uint32_t n = fdiv((uint32_t)m, P.div_ij);
-      uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
-      uint32_t ii = fdiv(rem, P.div_j);
-      uint32_t jj = rem - ii * (uint32_t)P.Mj;
-      int64_t orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
-      *reinterpret_cast<v4i*>(P.out + orow * P.Nout + col) =
-          *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+      int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
+      if (!P.dense) {    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+        uint32_t n = fdiv((uint32_t)m, P.div_ij);
+        uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+        uint32_t ii = fdiv(rem, P.div_j);
+        uint32_t jj = rem - ii * (uint32_t)P.Mj;
+        orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+      }
+      v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+      if (P.addend != nullptr) {  // fused residual-gradient sum (block input of a residual block)
+        f8 a = unpack8(__builtin_bit_cast(uint4, v));
+        f8 b = unpack8(*reinterpret_cast<const uint4*>(P.addend + orow * P.Nout + col));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
+        v = __builtin_bit_cast(v4i, pack8(a));
+      }
+      *reinterpret_cast<v4i*>(P.out + orow * P.Nout + col) = v;
     }
   }
 }
@@ -373,19 +388,21 @@ __device__ __forceinline__ v4i cat_frag(v4s_t lo, v4s_t hi) {
 template <int BMG, int BNG>
 struct TnCfg {
   static constexpr int NT = 256;
-  static constexpr int A_PT = 64 * (BMG / 8) / NT;   // chunks per thread
-  static constexpr int B_PT = 64 * (BNG / 8) / NT;
-  static constexpr int TILE_BYTES = 64 * 256;        // one [64][<=128] tile, 256-B pitch
+  static constexpr int TILE_BYTES = 64 * 256;        // one [64 m][<=128 col] tile, 256-B pitch
   static constexpr int SMEM = 2 * 2 * TILE_BYTES;    // 2 buffers x (A, B)
   static constexpr int TM = BMG / 2 / 16;            // 2x2 waves
   static constexpr int TN = BNG / 2 / 16;
+  static constexpr int PW = 16 / 4;                  // 1-KiB DMA instructions per wave per tile
 };
 
+// Main loop as igemm_nt (LDS-DMA, source-side swizzle, 2 buffers, one barrier per K-step).  A DMA
+// wave instruction covers 4 rows (m) x 256 B; lane l fetches row 4g + (l>>4), slot l&15 holding
+// chunk (l&15) ^ (swz(m)<<1).  With BMG = 64 the upper half of each 256-B row is fetched but never
+// read (keeps the one image layout for both tile widths).
 template <int BMG, int BNG, bool ATOMIC>
 __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   using CFG = TnCfg<BMG, BNG>;
-  constexpr int TM = CFG::TM, TN = CFG::TN;
-  constexpr int ACH = BMG / 8, BCH = BNG / 8;  // chunks per LDS row
+  constexpr int TM = CFG::TM, TN = CFG::TN, PW = CFG::PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Ncols + BNG - 1) / BNG;
@@ -398,68 +415,62 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
 
   const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
 
-  // A chunks: q = t + 256 i -> m-row q / ACH, chunk q % ACH (fixed kout columns per thread)
-  const int a_c = t % ACH;
-  const int a_r = t / ACH;
-  constexpr int A_RSTEP = 256 / ACH;
-  const int a_col = k0 + a_c * 8;
-  const bool a_colok = a_col < P.Kout;
-  // B chunks: fixed column chunk per thread -> fixed (tap, channel)
-  const int b_c = t % BCH;
-  const int b_r = t / BCH;
-  constexpr int B_RSTEP = 256 / BCH;
-  const int b_col = c0 + b_c * 8;
-  const bool b_colok = b_col < P.Ncols;
-  int b_tr = 0, b_ts = 0, b_ch = 0;
-  {
-    int tap = b_col / P.C;
-    b_ch = b_col - tap * P.C;
-    b_tr = tap / P.S;
-    b_ts = tap - b_tr * P.S;
+  const int lrow = lane >> 4, lslot = lane & 15;
+  int rows[PW], chk[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    rows[i] = (wid * PW + i) * 4 + lrow;                       // m row within the 64-row tile
+    const int sw = (rows[i] & 3) | (((rows[i] >> 3) & 1) << 2);
+    chk[i] = lslot ^ (sw << 1);                                 // source chunk for this slot
   }
-  const int b_dh = b_tr - P.pad, b_dw = b_ts - P.pad;
+  // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel)
+  int a_col[PW], b_dh[PW], b_dw[PW], b_ch[PW];
+  bool b_ok[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    a_col[i] = k0 + chk[i] * 8;
+    if (chk[i] * 8 >= BMG) a_col[i] = P.Kout;  // unused upper half (BMG = 64): force OOB
+    const int col = c0 + chk[i] * 8;
+    b_ok[i] = col < P.Ncols;
+    const int tap = col / P.C;
+    b_ch[i] = col - tap * P.C;
+    const int r = tap / P.S;
+    b_dh[i] = r - P.pad;
+    b_dw[i] = (tap - r * P.S) - P.pad;
+  }
 
-  v4i ra_reg[CFG::A_PT], rb_reg[CFG::B_PT];
-  auto load_tiles = [&](int step) {
+  auto issue = [&](int step, int buf) {
+    char* As = smem + buf * 2 * CFG::TILE_BYTES;
+    char* Bs = As + CFG::TILE_BYTES;
     const int mb = step * 64;
 #pragma unroll
-    for (int i = 0; i < CFG::A_PT; ++i) {
-      int m = mb + a_r + A_RSTEP * i;
-      bool ok = a_colok && m < P.Mred;
-      uint32_t off = ok ? (uint32_t)(((int64_t)m * P.Kout + a_col) * 2) : OOB;
-      ra_reg[i] = buf_load16(rdy, off);
+    for (int i = 0; i < PW; ++i) {
+      const int m = mb + rows[i];
+      bool ok = a_col[i] < P.Kout && m < P.Mred;
+      uint32_t off = ok ? (uint32_t)(((int64_t)m * P.Kout + a_col[i]) * 2) : OOB;
+      glds16(rdy, As + (wid * PW + i) * 1024, off);
     }
 #pragma unroll
-    for (int i = 0; i < CFG::B_PT; ++i) {
-      int m = mb + b_r + B_RSTEP * i;
+    for (int i = 0; i < PW; ++i) {
+      const int m = mb + rows[i];
       uint32_t off = OOB;
-      if (b_colok && m < P.Mred) {
+      if (b_ok[i] && m < P.Mred) {
         uint32_t n = fdiv((uint32_t)m, P.div_hw);
         uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
         uint32_t ho = fdiv(rem, P.div_w);
         uint32_t wo = rem - ho * (uint32_t)P.Wo;
-        int h = (int)ho * P.stride + b_dh, w = (int)wo * P.stride + b_dw;
+        int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride + b_dw[i];
         if ((unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W)
-          off = (uint32_t)(((((int)n * P.H + h) * P.W + w) * P.C + b_ch) * 2);
+          off = (uint32_t)(((((int)n * P.H + h) * P.W + w) * P.C + b_ch[i]) * 2);
       }
-      rb_reg[i] = buf_load16(rx, off);
+      glds16(rx, Bs + (wid * PW + i) * 1024, off);
     }
   };
-  auto store_tiles = [&](int buf) {
-    char* As = smem + buf * 2 * CFG::TILE_BYTES;
-    char* Bs = As + CFG::TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < CFG::A_PT; ++i)
-      *reinterpret_cast<v4i*>(As + swz256(a_r + A_RSTEP * i, a_c)) = ra_reg[i];
-#pragma unroll
-    for (int i = 0; i < CFG::B_PT; ++i)
-      *reinterpret_cast<v4i*>(Bs + swz256(b_r + B_RSTEP * i, b_c)) = rb_reg[i];
-  };
 
-  const int wid = t >> 6, lane = t & 63;
   const int wm = wid & 1, wn = wid >> 1;
   const int li = lane & 15, g = lane >> 4;  // group g covers k rows 8g..8g+7
   // tr-read address pieces: lane 4q+p of a group -> row q, columns 4p..4p+3
@@ -476,14 +487,12 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
     return base + swz256(row, col >> 3) + ((col & 7) << 1);
   };
 
-  if (s_begin < s_end) {
-    load_tiles(s_begin);
-    store_tiles(0);
-  }
+  if (s_begin < s_end) issue(s_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int step = s_begin; step < s_end; ++step) {
     const int cur = (step - s_begin) & 1;
-    if (step + 1 < s_end) load_tiles(step + 1);
+    if (step + 1 < s_end) issue(step + 1, cur ^ 1);
     const char* As = smem + cur * 2 * CFG::TILE_BYTES;
     const char* Bs = As + CFG::TILE_BYTES;
 #pragma unroll
@@ -509,7 +518,7 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    if (step + 1 < s_end) store_tiles(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -573,7 +582,12 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), CFG::SMEM, st, a);
+  // a single-step K loop never touches the second pipeline buffer: halve the LDS request so
+  // more blocks fit per CU (these short-K 1x1 convs are bound by their epilogue stores)
+  const int nk = C64 ? a.ntaps * (a.CA / 64) : (a.Kg + 63) / 64;
+  int smem = CFG::SMEM;
+  if (nk <= 1) smem = std::max(CFG::PIPE_BYTES / 2, CFG::EPI_BYTES);
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), smem, st, a);
   check_launch("igemm_nt");
 }
 
@@ -613,6 +627,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   fill_common(a, s.Ho, s.Wo);
   a.ash = s.stride; a.asw = s.stride; a.aoff_h = -s.pad; a.aoff_w = -s.pad;
   a.OH = s.Ho; a.OW = s.Wo; a.osh = 1; a.osw = 1; a.oph = 0; a.opw = 0;
+  a.dense = 1;
   a.ntaps = s.R * s.S;
   if (a.ntaps > MAX_TAPS) throw std::runtime_error("conv_fwd: too many taps");
   for (int r = 0; r < s.R; ++r)
@@ -630,14 +645,14 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   }
 }
 
-void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvShape& s,
-                       hipStream_t st) {
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
+                       const ConvShape& s, hipStream_t st) {
   if (s.K % 64 != 0) throw std::runtime_error("conv_dgrad: output channels must be a multiple of 64");
   const int str = s.stride;
   for (int ph = 0; ph < str; ++ph)
     for (int pw = 0; pw < str; ++pw) {
       NtArgs a{};
-      a.a = dy; a.b = wt; a.out = dx; a.part = nullptr;
+      a.a = dy; a.b = wt; a.out = dx; a.addend = addend; a.part = nullptr;
       a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
       a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * 2);
       a.HA = s.Ho; a.WA = s.Wo; a.CA = s.K;
@@ -649,6 +664,7 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
       fill_common(a, Mi, Mj);
       a.ash = 1; a.asw = 1; a.aoff_h = 0; a.aoff_w = 0;
       a.OH = s.H; a.OW = s.W; a.osh = str; a.osw = str; a.oph = ph; a.opw = pw;
+      a.dense = (str == 1);
       // taps of this parity class: (ph + pad - r) % str == 0 -> ho = i + (ph + pad - r)/str
       int nt = 0;
       for (int r = 0; r < s.R; ++r) {

@@ -30,9 +30,10 @@ struct ConvShape {
 int conv_fwd_group_rows(int M, int Nout);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
                      const ConvShape& s, hipStream_t st);
-// dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (all stride/pad combos, parity classes)
-void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const ConvShape& s,
-                       hipStream_t st);
+// dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);
+// all stride/pad combos (stride > 1 as stride^2 parity classes)
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
+                       const ConvShape& s, hipStream_t st);
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);

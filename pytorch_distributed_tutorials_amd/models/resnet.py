@@ -65,6 +65,9 @@ class BasicBlock(nn.Module):
         return self.relu(out + identity)
 
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:  # one fused autograd node per block on the device path
+            ds = (self.downsample[0], self.downsample[1]) if self.downsample is not None else None
+            return ops.residual_block(x, [(self.conv1, self.bn1), (self.conv2, self.bn2)], ds)
         out = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
         identity = x
         if self.downsample is not None:
@@ -99,6 +102,10 @@ class Bottleneck(nn.Module):
         return self.relu(out + identity)
 
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:  # one fused autograd node per block on the device path
+            ds = (self.downsample[0], self.downsample[1]) if self.downsample is not None else None
+            return ops.residual_block(
+                x, [(self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)], ds)
         identity = x
         if self.downsample is not None:
             identity = ops.conv_bn(x, self.downsample[0], self.downsample[1], relu=False)

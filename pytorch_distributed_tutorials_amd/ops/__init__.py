@@ -13,6 +13,7 @@ from .fused import (  # noqa: F401
     cross_entropy,
     image_to_nhwc,
     maxpool3x3s2,
+    residual_block,
     set_cpu_activation_dtype,
     top1_correct,
 )

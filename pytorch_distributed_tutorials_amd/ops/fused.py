@@ -231,3 +231,142 @@ def top1_correct(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     if logits.is_cuda:
         return native().top1_correct(logits.contiguous(), labels.contiguous())
     return ref.top1_correct(logits, labels)
+
+
+# ----------------------------------------------------------------------------
+# whole residual block (device path): one autograd node per Bottleneck/BasicBlock
+# ----------------------------------------------------------------------------
+def _bn_prepare(bn: nn.BatchNorm2d):
+    """(training, momentum, eps) for one BN call; bumps num_batches_tracked like torch."""
+    training = bn.training or not bn.track_running_stats
+    momentum = bn.momentum
+    if training and bn.track_running_stats:
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+        if momentum is None:
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    return training, (momentum if momentum is not None else 0.0), bn.eps
+
+
+def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual):
+    k, _, r, s = w.shape
+    n, h, wd, cx = x.shape
+    count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
+    wk = C.pack_weight(w, cx)
+    y, part = C.conv_fwd(x, wk, stride, pad, training)
+    if training:
+        stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
+    else:
+        stats = C.bn_eval_params(rm, rv, gamma, beta, float(eps))
+    mean, invstd, scale, shift = stats.unbind(0)
+    z = C.bn_act_fwd(y, scale, shift, residual, relu)
+    return z, y, mean, invstd
+
+
+class _ResidualBlock(torch.autograd.Function):
+    """z = relu(unit_n(...unit_1(x)) + shortcut(x)) with unit = conv -> BN -> (ReLU).
+
+    One autograd node per block lets backward fuse across units: the shortcut
+    gradient is summed into the block-input gradient inside the first conv's
+    dgrad epilogue (no separate add kernel), and units are processed in one
+    straight-line sequence of native launches.
+    tensors = per unit (w, gamma, beta, running_mean, running_var), chain units
+    first, then the downsample unit if present.
+    """
+
+    @staticmethod
+    def forward(ctx, x, spec, *tensors):
+        C = native()
+        chain, ds_cfg = spec
+        nch = len(chain)
+        saved = [x]
+        # shortcut first (it only needs x) so its output can be freed into the tail's add
+        if ds_cfg is not None:
+            w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
+            st, pd, tr, mo, ep = ds_cfg
+            res, y_ds, mu_ds, is_ds = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None)
+        else:
+            res = x
+        h = x
+        outs = []
+        for i, (st, pd, tr, mo, ep) in enumerate(chain):
+            w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
+            last = i == nch - 1
+            z, y, mu, istd = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
+                                       res if last else None)
+            outs.append((z, y, mu, istd))
+            h = z
+        for z, y, mu, istd in outs:
+            saved += [z, y, mu, istd]
+        if ds_cfg is not None:
+            saved += [y_ds, mu_ds, is_ds]
+        ctx.save_for_backward(*saved, *tensors)
+        ctx.spec = spec
+        ctx.ntensors = len(tensors)
+        return h
+
+    @staticmethod
+    def backward(ctx, dz):
+        C = native()
+        chain, ds_cfg = ctx.spec
+        nch = len(chain)
+        sv = ctx.saved_tensors
+        x = sv[0]
+        units = [sv[1 + 4 * i:5 + 4 * i] for i in range(nch)]
+        pos = 1 + 4 * nch
+        if ds_cfg is not None:
+            y_ds, mu_ds, is_ds = sv[pos:pos + 3]
+            pos += 3
+        tensors = sv[pos:]
+        grads = [None] * ctx.ntensors
+        dz = dz.contiguous()
+        det = deterministic()
+        g_short = None
+        for i in reversed(range(nch)):
+            st, pd, tr, mo, ep = chain[i]
+            z, y, mu, istd = units[i]
+            w, gamma = tensors[5 * i], tensors[5 * i + 1]
+            xin = x if i == 0 else units[i - 1][0]
+            last = i == nch - 1
+            sums = C.bn_act_bwd_reduce(dz, z, y, mu, True)
+            dy, dres = C.bn_act_bwd_apply(dz, z, y, mu, istd, gamma, sums, True, tr, last)
+            grads[5 * i + 1] = sums[1] * istd
+            grads[5 * i + 2] = sums[0]
+            grads[5 * i] = C.conv_wgrad(dy, xin, list(w.shape), st, pd, det).to(w.dtype)
+            if last:
+                g_short = dres
+            if i > 0:
+                dz = C.conv_dgrad(dy, w, list(xin.shape), st, pd)
+            else:
+                # shortcut gradient: identity -> g_short itself; projection -> its dgrad
+                if ds_cfg is not None:
+                    st2, pd2, tr2, _, _ = ds_cfg
+                    wds, gds = tensors[5 * nch], tensors[5 * nch + 1]
+                    sums_ds = C.bn_act_bwd_reduce(g_short, g_short, y_ds, mu_ds, False)
+                    dy_ds, _ = C.bn_act_bwd_apply(g_short, g_short, y_ds, mu_ds, is_ds, gds, sums_ds,
+                                                  False, tr2, False)
+                    grads[5 * nch + 1] = sums_ds[1] * is_ds
+                    grads[5 * nch + 2] = sums_ds[0]
+                    grads[5 * nch] = C.conv_wgrad(dy_ds, x, list(wds.shape), st2, pd2, det).to(wds.dtype)
+                    addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2)
+                else:
+                    addend = g_short
+                dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend) if ctx.needs_input_grad[0] else None
+        return (dz, None, *grads)
+
+
+def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
+    """Device path of a ResNet block: ``chain`` = [(conv, bn), ...] (ReLU after each BN, the
+    shortcut added before the last ReLU), ``downsample`` = (conv, bn) or None."""
+    spec_chain, tensors = [], []
+    for conv, bn in chain:
+        tr, mo, ep = _bn_prepare(bn)
+        spec_chain.append((conv.stride[0], conv.padding[0], tr, mo, ep))
+        tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    ds_spec = None
+    if downsample is not None:
+        conv, bn = downsample
+        tr, mo, ep = _bn_prepare(bn)
+        ds_spec = (conv.stride[0], conv.padding[0], tr, mo, ep)
+        tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    return _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec), *tensors)

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen via torch")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="single shape CxHxWxKxRxSxstridexpad")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda:0")
@@ -73,7 +74,11 @@ def main():
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "t_fwd": 0.0, "t_dgrad": 0.0, "t_wgrad": 0.0, "flop": 0.0}
     print("C,H,W,K,R,S,st,pd,count,M,N,K_gemm,fwd_ms,fwd_TF,dgrad_ms,dgrad_TF,wgrad_ms,wgrad_TF"
           + (",torch_fwd_ms,torch_dgrad_ms,torch_wgrad_ms" if a.torch else ""))
-    for (c, h, w, k, r, s, st, pd), cnt in conv_shapes(a.arch, N, a.image).items():
+    shapes = conv_shapes(a.arch, N, a.image)
+    if a.only:
+        want = tuple(int(v) for v in a.only.split("x"))
+        shapes = OrderedDict([(want, 1)])
+    for (c, h, w, k, r, s, st, pd), cnt in shapes.items():
         cx = c if c % 8 == 0 else 8
         ho = (h + 2 * pd - r) // st + 1
         wo = (w + 2 * pd - s) // st + 1

@@ -1,0 +1,29 @@
+#!/bin/bash
+# PMC counters for a few conv shapes (kernel-trace + pmc only; no sys/hip tracing).
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=$R/gpurun_out/pmc; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
+pick() { python3 - "$O/counters_list.txt" "$@" <<'PY'
+import sys, re
+txt = open(sys.argv[1]).read()
+have = [c for c in sys.argv[2:] if re.search(r'\b' + re.escape(c) + r'\b', txt)]
+print(" ".join(have))
+PY
+}
+SET1=$(pick SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT)
+SET2=$(pick SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE)
+SET3=$(pick TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCC_EA0_RDREQ_sum)
+echo "SET1=$SET1" > $O/sets.txt; echo "SET2=$SET2" >> $O/sets.txt; echo "SET3=$SET3" >> $O/sets.txt
+for shape in 64x56x56x64x3x3x1x1 256x14x14x256x3x3x1x1 64x56x56x256x1x1x1x0; do
+  i=0
+  for S in "$SET1" "$SET2" "$SET3"; do
+    i=$((i+1))
+    [ -z "$S" ] && continue
+    timeout -k 10 200 rocprofv3 --kernel-trace --pmc $S --output-format csv -d $O/${shape}_s$i -o run -- python3 $R/scripts/bench_conv.py --only $shape --iters 3 > $O/${shape}_s$i.log 2>&1
+    rc=$?; echo "$shape set$i rc=$rc" >> $O/status.txt
+    [ $rc -eq 0 ] || exit $rc
+  done
+done
+exit 0

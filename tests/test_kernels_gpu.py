@@ -259,3 +259,37 @@ def test_resnet18_native_matches_torch(gpu, native_ext):
         assert cos > 0.85, f"{name}: cosine {cos}"
     for (name, bt), (_, bn) in zip(mt.named_buffers(), mn.named_buffers()):
         assert torch.allclose(bn.float().cpu(), bt.float(), atol=5e-2, rtol=5e-2), name
+
+
+@pytest.mark.parametrize("arch,idx", [("resnet50", (1, 0)), ("resnet50", (1, 1)), ("resnet18", (2, 0))])
+def test_residual_block_matches_unit_path(gpu, native_ext, arch, idx):
+    """The fused block autograd node == the per-unit conv_bn composition (same kernels)."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    torch.manual_seed(0)
+    m = build_model(arch).to(gpu).set_impl("native")
+    blk = getattr(m, f"layer{idx[0]}")[idx[1]]
+    blk2 = copy.deepcopy(blk)
+    cin = blk.conv1.in_channels
+    x = torch.randn(4, 16, 16, cin, device=gpu).to(torch.bfloat16).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    out = blk.forward_native(x)                       # fused block node
+    chain = [(blk2.conv1, blk2.bn1), (blk2.conv2, blk2.bn2)]
+    if hasattr(blk2, "conv3"):
+        chain.append((blk2.conv3, blk2.bn3))
+    ident = x2
+    if blk2.downsample is not None:
+        ident = ops.conv_bn(x2, blk2.downsample[0], blk2.downsample[1], relu=False)
+    h = x2
+    for i, (c, b) in enumerate(chain):
+        h = ops.conv_bn(h, c, b, relu=True, residual=ident if i == len(chain) - 1 else None)
+    assert torch.equal(out, h)
+    g = torch.randn(out.shape, device=gpu).to(torch.bfloat16)
+    out.backward(g)
+    h.backward(g)
+    assert _rel_err(x.grad, x2.grad) < 1e-2
+    for (n1, p1), (n2, p2) in zip(blk.named_parameters(), blk2.named_parameters()):
+        assert _rel_err(p1.grad, p2.grad) < 1e-2, n1
+    for b1, b2 in zip(blk.buffers(), blk2.buffers()):
+        assert torch.equal(b1, b2)
