@@ -130,7 +130,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
 
 // dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
-                  int64_t pad, bool deterministic) {
+                  int64_t pad, bool deterministic, const std::optional<Tensor>& out) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(x, "x");
   TORCH_CHECK(ws.size() == 4, "weight shape must be [K,C,R,S]");
@@ -140,11 +140,26 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
   auto s = shape_of(x.size(0), x.size(1), x.size(2), Cx, K, R, S, stride, pad);
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && K == dy.size(3), "wgrad: dy shape mismatch");
   auto fopt = x.options().dtype(at::kFloat);
-  auto dwp = at::empty({K, R, S, Cx}, fopt);
   size_t wsn = pdt::conv_wgrad_ws_floats(s, deterministic);
   Tensor wsb = wsn ? at::empty({(int64_t)wsn}, fopt) : Tensor();
+  if (out.has_value() && out->defined()) {
+    // accumulate into a caller-owned [K,C,R,S] fp32 tensor whose memory is KRSC-contiguous
+    // (a channels_last view of the flat gradient buffer)
+    const Tensor& o = *out;
+    TORCH_CHECK(Cx == C, "in-place wgrad needs unpadded input channels");
+    TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
+                o.size(2) == R && o.size(3) == S, "wgrad out: bad shape/dtype");
+    // KRSC-dense: strides (RSC, 1, SC, C); a size-1 dim may carry any stride
+    const int64_t want[4] = {(int64_t)R * S * C, 1, (int64_t)S * C, (int64_t)C};
+    for (int d = 0; d < 4; ++d)
+      TORCH_CHECK(o.size(d) == 1 || o.stride(d) == want[d], "wgrad out must be channels_last (KRSC) dense");
+    pdt::launch_conv_wgrad(cbf(dy), cbf(x), o.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
+                           s, deterministic, true, cur_stream(x));
+    return o;
+  }
+  auto dwp = at::empty({K, R, S, Cx}, fopt);
   pdt::launch_conv_wgrad(cbf(dy), cbf(x), dwp.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
-                         s, deterministic, cur_stream(x));
+                         s, deterministic, false, cur_stream(x));
   Tensor krsc = Cx == C ? dwp : dwp.narrow(3, 0, C).contiguous();
   return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
 }
@@ -198,37 +213,53 @@ Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
   return z;
 }
 
-Tensor bn_act_bwd_reduce(const Tensor& dz, const Tensor& z, const Tensor& y, const Tensor& mean,
-                         bool relu) {
+Tensor bn_act_bwd_reduce(const Tensor& dz, const Tensor& z, const Tensor& y, const Tensor& stats,
+                         int64_t mask, const std::optional<Tensor>& dgamma,
+                         const std::optional<Tensor>& dbeta) {
   check_bf16_nhwc(dz, "dz");
   check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(dz.get_device());
   int K = y.size(3);
   TORCH_CHECK(256 % (K / 8) == 0, "bn backward: channels must divide 2048 and be a power of two");
+  TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
+  if (mask == 1) check_bf16_nhwc(z, "z");
   int64_t M = y.numel() / K;
   auto fopt = y.options().dtype(at::kFloat);
   auto ws = at::empty({(int64_t)pdt::bn_bwd_ws_floats(M, K)}, fopt);
   auto sums = at::empty({2, K}, fopt);
-  pdt::launch_bn_act_bwd_reduce(cbf(dz), cbf(z), cbf(y), mean.data_ptr<float>(), relu, M, K,
-                                ws.data_ptr<float>(), sums.data_ptr<float>(), cur_stream(y));
+  float* dg = nullptr;
+  float* db = nullptr;
+  if (dgamma.has_value() && dgamma->defined()) {
+    TORCH_CHECK(dbeta.has_value() && dbeta->defined(), "dgamma and dbeta go together");
+    TORCH_CHECK(dgamma->numel() == K && dbeta->numel() == K && dgamma->is_contiguous() &&
+                dbeta->is_contiguous() && dgamma->scalar_type() == at::kFloat, "bad dgamma/dbeta");
+    dg = dgamma->data_ptr<float>();
+    db = dbeta->data_ptr<float>();
+  }
+  pdt::launch_bn_act_bwd_reduce(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
+                                (int)mask, M, K, ws.data_ptr<float>(), sums.data_ptr<float>(), dg, db,
+                                cur_stream(y));
   return sums;
 }
 
 std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, const Tensor& y,
-                                            const Tensor& mean, const Tensor& invstd,
-                                            const Tensor& gamma, const Tensor& sums, bool relu,
-                                            bool training, bool want_dres) {
+                                            const Tensor& stats, const Tensor& gamma,
+                                            const Tensor& sums, int64_t mask, bool training,
+                                            bool want_dres) {
   check_bf16_nhwc(dz, "dz");
+  check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(dz.get_device());
   int K = y.size(3);
+  TORCH_CHECK(256 % (K / 8) == 0, "bn backward: channels must divide 2048 and be a power of two");
+  TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
+  if (mask == 1) check_bf16_nhwc(z, "z");
   int64_t M = y.numel() / K;
   auto dy = at::empty_like(dz);
   Tensor dres;
   if (want_dres) dres = at::empty_like(dz);
-  pdt::launch_bn_act_bwd_apply(cbf(dz), cbf(z), cbf(y), mean.data_ptr<float>(),
-                               invstd.data_ptr<float>(), gamma.data_ptr<float>(),
-                               sums.data_ptr<float>(), relu, training, M, K, bf(dy),
-                               want_dres ? bf(dres) : nullptr, cur_stream(dz));
+  pdt::launch_bn_act_bwd_apply(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
+                               gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)mask, training,
+                               M, K, bf(dy), want_dres ? bf(dres) : nullptr, cur_stream(dz));
   return {dy, dres};
 }
 
@@ -330,12 +361,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("deterministic") = false);
+        py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_params", &bn_eval_params);
   m.def("bn_act_fwd", &bn_act_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"));
-  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce);
+  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("y"),
+        py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
@@ -379,6 +411,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("average") = true, py::arg("wire_dtype") = "fp32")
       .def("prepare_for_backward", &pdt::Reducer::prepare_for_backward,
            py::call_guard<py::gil_scoped_release>())
+      .def("mark_ready_external", &pdt::Reducer::mark_ready_external)
       .def("set_enabled", &pdt::Reducer::set_enabled)
       .def_property_readonly("enabled", &pdt::Reducer::enabled)
       .def_property_readonly("num_buckets", &pdt::Reducer::num_buckets)

@@ -103,6 +103,23 @@ struct ReducerState {
     }
   }
 
+  // a parameter's gradient is final in its flat view (from its AccumulateGrad hook, or written
+  // in place by a fused native backward that then calls mark_ready_external)
+  void on_ready(int64_t idx) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!enabled || !expecting) return;
+    if (!callback_queued) {
+      callback_queued = true;
+      std::weak_ptr<ReducerState> w2 = self;
+      torch::autograd::Engine::get_default_engine().queue_callback([w2]() {
+        if (auto s2 = w2.lock()) s2->finalize();
+      });
+    }
+    mark_param(idx, /*zero_if_missing=*/false);
+  }
+
+  std::weak_ptr<ReducerState> self;
+
   void finalize() {
     std::lock_guard<std::mutex> lk(mu);
     // parameters that received no gradient this iteration (unused in forward): zero views
@@ -148,6 +165,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   st_->reset_counters();
 
   std::weak_ptr<ReducerState> weak = st_;
+  st_->self = weak;
   for (size_t i = 0; i < st_->params.size(); ++i) {
     auto acc = torch::autograd::impl::grad_accumulator(st_->params[i]);
     if (!acc) throw std::runtime_error("Reducer: parameter has no grad accumulator (requires_grad?)");
@@ -155,18 +173,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
     acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
         [weak, idx](const torch::autograd::variable_list& outputs,
                     const torch::autograd::variable_list& /*inputs*/) {
-          auto s = weak.lock();
-          if (!s) return outputs;
-          std::lock_guard<std::mutex> lk(s->mu);
-          if (!s->enabled || !s->expecting) return outputs;
-          if (!s->callback_queued) {
-            s->callback_queued = true;
-            std::weak_ptr<ReducerState> w2 = s;
-            torch::autograd::Engine::get_default_engine().queue_callback([w2]() {
-              if (auto s2 = w2.lock()) s2->finalize();
-            });
-          }
-          s->mark_param(idx, /*zero_if_missing=*/false);
+          if (auto s = weak.lock()) s->on_ready(idx);
           return outputs;
         }));
     st_->accumulators.push_back(std::move(acc));
@@ -180,6 +187,13 @@ void Reducer::prepare_for_backward() {
   st_->reset_counters();
   st_->expecting = st_->enabled;
   st_->callback_queued = false;
+}
+
+void Reducer::mark_ready_external(const std::vector<int64_t>& idx) {
+  for (int64_t i : idx) {
+    if (i < 0 || i >= (int64_t)st_->params.size()) throw std::runtime_error("mark_ready_external: bad index");
+    st_->on_ready(i);
+  }
 }
 
 void Reducer::set_enabled(bool enabled) {

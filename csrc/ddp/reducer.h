@@ -43,6 +43,8 @@ class Reducer {
   ~Reducer();
 
   void prepare_for_backward();
+  // gradients already accumulated into their flat views by a fused native backward
+  void mark_ready_external(const std::vector<int64_t>& idx);
   void set_enabled(bool enabled);
   bool enabled() const;
   int64_t num_buckets() const;

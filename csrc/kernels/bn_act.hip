@@ -12,7 +12,11 @@
 namespace pdt {
 
 // ------------------------------------------------------------------ finalize
-// Stage 1: block (cx, p) merges groups [p*GPB, (p+1)*GPB) for 32 channels.
+// Group g (grows rows, the last one possibly fewer) carries (s_g, q_g) = (sum, M2 about its mean).
+// With S = sum s_g, A = sum q_g, B = sum s_g^2/n_g:  mean = S/M,  M2 = A + B - S^2/M
+// (exact decomposition of the total sum of squares; only plain sums -> fully parallel, no
+// serial divide chain).  Stage 1: block (32 channels, partition p of FIN_GPB groups);
+// stage 2: per channel sum over partitions, fixed order (deterministic).
 constexpr int FIN_CH = 32;
 constexpr int FIN_ROWS = 8;                 // threads per channel in a block
 constexpr int FIN_GPB = FIN_ROWS * 32;      // groups per block
@@ -20,26 +24,29 @@ constexpr int FIN_GPB = FIN_ROWS * 32;      // groups per block
 __global__ void __launch_bounds__(256) bn_finalize_stage1(const float* __restrict__ part, int ngroups,
                                                           int grows, int M, int K,
                                                           float* __restrict__ ws) {
-  __shared__ float sn[FIN_ROWS][FIN_CH], smu[FIN_ROWS][FIN_CH], sm2[FIN_ROWS][FIN_CH];
-  int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
-  int k = blockIdx.x * FIN_CH + tx;
-  int g0 = blockIdx.y * FIN_GPB;
-  int g1 = min(ngroups, g0 + FIN_GPB);
-  float n = 0.f, mu = 0.f, m2 = 0.f;
+  __shared__ float sS[FIN_ROWS][FIN_CH + 1], sA[FIN_ROWS][FIN_CH + 1], sB[FIN_ROWS][FIN_CH + 1];
+  const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
+  const int k = blockIdx.x * FIN_CH + tx;
+  const int g0 = blockIdx.y * FIN_GPB;
+  const int g1 = min(ngroups, g0 + FIN_GPB);
+  float S = 0.f, A = 0.f, B = 0.f;
   if (k < K) {
+#pragma unroll 4
     for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
-      float cnt = (float)min(grows, M - g * grows);
-      float s = part[((int64_t)g * 2 + 0) * K + k];
-      float q = part[((int64_t)g * 2 + 1) * K + k];
-      chan_merge(n, mu, m2, cnt, s / cnt, q);
+      const float cnt = (float)min(grows, M - g * grows);
+      const float sg = part[((int64_t)g * 2 + 0) * K + k];
+      const float qg = part[((int64_t)g * 2 + 1) * K + k];
+      S += sg;
+      A += qg;
+      B = fmaf(sg, sg / cnt, B);
     }
   }
-  sn[ty][tx] = n; smu[ty][tx] = mu; sm2[ty][tx] = m2;
+  sS[ty][tx] = S; sA[ty][tx] = A; sB[ty][tx] = B;
   __syncthreads();
   if (ty == 0 && k < K) {
-    for (int r = 1; r < FIN_ROWS; ++r) chan_merge(n, mu, m2, sn[r][tx], smu[r][tx], sm2[r][tx]);
+    for (int r = 1; r < FIN_ROWS; ++r) { S += sS[r][tx]; A += sA[r][tx]; B += sB[r][tx]; }
     float* o = ws + ((int64_t)blockIdx.y * 3) * K;
-    o[k] = n; o[K + k] = mu; o[2 * K + k] = m2;
+    o[k] = S; o[K + k] = A; o[2 * K + k] = B;
   }
 }
 
@@ -52,11 +59,14 @@ __global__ void __launch_bounds__(256) bn_finalize_stage2(const float* __restric
                                                           float* __restrict__ out) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
-  float n = 0.f, mu = 0.f, m2 = 0.f;
+  float S = 0.f, A = 0.f, B = 0.f;
+#pragma unroll 4
   for (int p = 0; p < P; ++p) {
     const float* o = ws + ((int64_t)p * 3) * K;
-    chan_merge(n, mu, m2, o[k], o[K + k], o[2 * K + k]);
+    S += o[k]; A += o[K + k]; B += o[2 * K + k];
   }
+  const float mu = S / (float)M;
+  const float m2 = fmaxf(A + B - S * mu, 0.f);
   float var = m2 / (float)M;
   float invstd = rsqrtf(var + eps);
   if (rm != nullptr) {
@@ -168,14 +178,32 @@ static int red_blocks(int64_t M) {
 
 size_t bn_bwd_ws_floats(int64_t M, int K) { return (size_t)red_blocks(M) * 2 * K; }
 
-template <bool RELU>
+// Relu-mask modes of the backward kernels: 0 = no ReLU, 1 = mask from the saved output z (z > 0),
+// 2 = mask recomputed from y (y*scale + shift > 0, bit-identical to the forward's fp32 math) --
+// used for units without a residual input so backward never reads z (saves 2 B/element/pass).
+template <int MASK>
+__device__ __forceinline__ float relu_grad(float g, float zv, float yv, float sc, float sh) {
+  if (MASK == 1) return zv > 0.f ? g : 0.f;
+  if (MASK == 2) return fmaf(yv, sc, sh) > 0.f ? g : 0.f;
+  return g;
+}
+
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// stats = [4][K]: mean, invstd, scale, shift (bn_finalize output)
+template <int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restrict__ dz,
                                                             const uint4* __restrict__ z,
                                                             const uint4* __restrict__ y,
-                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ stats,
                                                             int64_t M, int K8,
                                                             float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int K = K8 * 8;
   const int t = threadIdx.x;
   const int c8 = t % K8;
   const int rpi = 256 / K8;  // rows per iteration
@@ -183,24 +211,20 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
   int64_t rows_per_block = (M + gridDim.x - 1) / gridDim.x;
   int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   int64_t r1 = min(M, r0 + rows_per_block);
-  float mu[8];
-  {
-    float4 m0 = *reinterpret_cast<const float4*>(mean + c8 * 8);
-    float4 m1 = *reinterpret_cast<const float4*>(mean + c8 * 8 + 4);
-    mu[0] = m0.x; mu[1] = m0.y; mu[2] = m0.z; mu[3] = m0.w;
-    mu[4] = m1.x; mu[5] = m1.y; mu[6] = m1.z; mu[7] = m1.w;
-  }
+  float mu[8], sc[8], shf[8];
+  load8(stats + c8 * 8, mu);
+  if (MASK == 2) { load8(stats + 2 * K + c8 * 8, sc); load8(stats + 3 * K + c8 * 8, shf); }
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t r = r0 + roff; r < r1; r += rpi) {
     int64_t v = r * K8 + c8;
     f8 d = unpack8(dz[v]);
     f8 yy = unpack8(y[v]);
     f8 zz;
-    if (RELU) zz = unpack8(z[v]);
+    if (MASK == 1) zz = unpack8(z[v]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float g = d.v[j];
-      if (RELU) g = zz.v[j] > 0.f ? g : 0.f;
+      float g = relu_grad<MASK>(d.v[j], MASK == 1 ? zz.v[j] : 0.f, yy.v[j],
+                                MASK == 2 ? sc[j] : 0.f, MASK == 2 ? shf[j] : 0.f);
       sg[j] += g;
       sgx[j] = fmaf(g, yy.v[j] - mu[j], sgx[j]);
     }
@@ -219,7 +243,6 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
     __syncthreads();
   }
   if (roff == 0) {
-    int K = K8 * 8;
     float* o = ws + (int64_t)blockIdx.x * 2 * K;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = my[j]; o[K + c8 * 8 + j] = my[8 + j]; }
@@ -229,7 +252,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
 // block = 32 channels x 8 partial-lanes; each lane sums nb/8 stage-1 partials (independent
 // loads, pipelined), then an LDS combine.  Deterministic (fixed order).
 __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restrict__ ws, int nb,
-                                                            int K, float* __restrict__ sums) {
+                                                            int K, float* __restrict__ sums,
+                                                            const float* __restrict__ invstd,
+                                                            float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta) {
   __shared__ float sa[8][33], sb[8][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int k = blockIdx.x * 32 + tx;
@@ -248,56 +274,73 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restr
     for (int r = 1; r < 8; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
     sums[k] = a;       // sum g          (= dbeta)
     sums[K + k] = b;   // sum g*(y-mean) (dgamma = b*invstd)
+    if (dgamma != nullptr) {
+      dgamma[k] += b * invstd[k];
+      dbeta[k] += a;
+    }
   }
 }
 
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
-                              const float* mean, bool relu, int64_t M, int K, float* ws,
-                              float* sums, hipStream_t st) {
+                              const float* stats, int mask, int64_t M, int K, float* ws,
+                              float* sums, float* dgamma, float* dbeta, hipStream_t st) {
   int K8 = K / 8;
   int nb = red_blocks(M);
   size_t shmem = 256 * 16 * sizeof(float);
   auto DZ = reinterpret_cast<const uint4*>(dz);
   auto Z = reinterpret_cast<const uint4*>(z);
   auto Y = reinterpret_cast<const uint4*>(y);
-  if (relu)
-    hipLaunchKernelGGL(bn_bwd_reduce_stage1<true>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, mean, M, K8, ws);
+  if (mask == 1)
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<1>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
+  else if (mask == 2)
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<2>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_stage1<false>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, mean, M, K8, ws);
-  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K, sums);
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<0>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
+  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K, sums,
+                     stats + K, dgamma, dbeta);
 }
 
 // ------------------------------------------------------------- backward apply
-template <bool RELU, bool TRAIN, bool DRES>
+// Grid-stride with gridDim*256 a multiple of K/8, so every thread keeps one fixed 8-channel
+// group: the per-channel coefficients are computed once per thread, not per element.
+template <int MASK, bool TRAIN, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const uint4* __restrict__ dz, const uint4* __restrict__ z, const uint4* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ gamma, const float* __restrict__ sums, int64_t nvec, int K8,
-    float invM, uint4* __restrict__ dy, uint4* __restrict__ dres) {
+    const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ sums, int64_t nvec, int K8, float invM, uint4* __restrict__ dy,
+    uint4* __restrict__ dres) {
   const int K = K8 * 8;
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    int c0 = (int)(v % K8) * 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(tid % K8) * 8;
+  float k1[8], sgm[8], k2[8], mu[8], sc[8], shf[8];
+  {
+    float is[8], gm[8], s0[8], s1[8];
+    load8(stats + K + c0, is);
+    load8(gamma + c0, gm);
+    load8(stats + c0, mu);
+    load8(sums + c0, s0);
+    load8(sums + K + c0, s1);
+    if (MASK == 2) { load8(stats + 2 * K + c0, sc); load8(stats + 3 * K + c0, shf); }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k1[j] = gm[j] * is[j];
+      sgm[j] = s0[j] * invM;                 // mean of g
+      k2[j] = s1[j] * is[j] * is[j] * invM;  // mean of g*xhat, divided by std
+    }
+  }
+  for (int64_t v = tid; v < nvec; v += stride) {
     f8 d = unpack8(dz[v]);
     f8 zz, yy;
-    if (RELU) zz = unpack8(z[v]);
-    if (TRAIN) yy = unpack8(y[v]);
+    if (MASK == 1) zz = unpack8(z[v]);
+    if (TRAIN || MASK == 2) yy = unpack8(y[v]);
     f8 o, gr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      int c = c0 + j;
-      float g = d.v[j];
-      if (RELU) g = zz.v[j] > 0.f ? g : 0.f;
+      float g = relu_grad<MASK>(d.v[j], MASK == 1 ? zz.v[j] : 0.f, (TRAIN || MASK == 2) ? yy.v[j] : 0.f,
+                                MASK == 2 ? sc[j] : 0.f, MASK == 2 ? shf[j] : 0.f);
       gr.v[j] = g;
-      float is = invstd[c];
-      float k1 = gamma[c] * is;
-      if (TRAIN) {
-        float sg = sums[c] * invM;                 // mean of g
-        float k2 = sums[K + c] * is * is * invM;   // mean of g*xhat, divided by std
-        o.v[j] = k1 * (g - sg - (yy.v[j] - mean[c]) * k2);
-      } else {
-        o.v[j] = k1 * g;
-      }
+      o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
     }
     dy[v] = pack8(o);
     if (DRES) dres[v] = pack8(gr);
@@ -305,9 +348,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 }
 
 void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
-                             const float* mean, const float* invstd, const float* gamma,
-                             const float* sums, bool relu, bool training, int64_t M, int K,
-                             uint16_t* dy, uint16_t* dres, hipStream_t st) {
+                             const float* stats, const float* gamma, const float* sums, int mask,
+                             bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
+                             hipStream_t st) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
   dim3 g(ew_blocks(nvec)), b(256);
@@ -317,17 +360,16 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   auto DY = reinterpret_cast<uint4*>(dy);
   auto DR = reinterpret_cast<uint4*>(dres);
   float invM = 1.f / (float)M;
-#define PDT_BWD(RL, TR, DRS)                                                                     \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, TR, DRS>), g, b, 0, st, DZ, Z, Y, mean, invstd, \
-                     gamma, sums, nvec, K8, invM, DY, DR)
-  bool dr = dres != nullptr;
-  if (relu) {
-    if (training) { if (dr) PDT_BWD(true, true, true); else PDT_BWD(true, true, false); }
-    else { if (dr) PDT_BWD(true, false, true); else PDT_BWD(true, false, false); }
-  } else {
-    if (training) { if (dr) PDT_BWD(false, true, true); else PDT_BWD(false, true, false); }
-    else { if (dr) PDT_BWD(false, false, true); else PDT_BWD(false, false, false); }
-  }
+#define PDT_BWD(MK, TR, DRS)                                                                  \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, TR, DRS>), g, b, 0, st, DZ, Z, Y, stats, gamma, \
+                     sums, nvec, K8, invM, DY, DR)
+#define PDT_BWD_T(MK)                                                             \
+  if (training) { if (dres) PDT_BWD(MK, true, true); else PDT_BWD(MK, true, false); } \
+  else { if (dres) PDT_BWD(MK, false, true); else PDT_BWD(MK, false, false); }
+  if (mask == 1) { PDT_BWD_T(1) }
+  else if (mask == 2) { PDT_BWD_T(2) }
+  else { PDT_BWD_T(0) }
+#undef PDT_BWD_T
 #undef PDT_BWD
 }
 

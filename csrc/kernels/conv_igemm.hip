@@ -79,8 +79,6 @@ constexpr uint32_t OOB = 0x80000000u;  // any offset >= num_records reads 0
 // ============================================================================
 //                          NT implicit GEMM (fwd / dgrad)
 // ============================================================================
-constexpr int MAX_TAPS = 49;
-
 struct NtArgs {
   const uint16_t* a;   // activation source NHWC (x for fwd, dy for dgrad), CA channels
   const uint16_t* b;   // [Nout][Kg] k-contiguous
@@ -96,9 +94,10 @@ struct NtArgs {
   int ash, asw, aoff_h, aoff_w;     // A base coords: h0 = i*ash + aoff_h
   int OH, OW, osh, osw, oph, opw;   // out row = (n*OH + i*osh + oph)*OW + j*osw + opw
   int dense;           // output row == m (no scatter)
-  int ntaps;
-  int8_t tdr[MAX_TAPS], tds[MAX_TAPS];
-  int16_t tb[MAX_TAPS];
+  // taps of this launch form a grid (i < tnr, j < tns): filter tap (tr0 + i*tstep, ts0 + j*tstep),
+  // A-coordinate offset (dr0 + i*dstep, ds0 + j*dstep).  Closed form -> pure scalar math in the
+  // K loop (a per-tap table in kernel args would be read with vector loads every K-step).
+  int ntaps, tnr, tns, tr0, ts0, tstep, dr0, ds0, dstep;
 };
 
 // LDS image of a [rows][64] bf16 tile: 128-B rows, 16-B chunk XOR-swizzled by (row>>1)&7.
@@ -158,7 +157,9 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
 
   // A rows (pixels) and B rows (output channels) this lane fetches, fixed over the K loop
-  int a_pix[A_PW], a_h0[A_PW], a_w0[A_PW], a_c[A_PW];
+  // a_base: byte offset of (h0, w0, this lane's chunk) -- a tap adds the uniform scalar
+  // ((dr*WA + ds)*CA + chb)*2; only the bounds test on (h0+dr, w0+ds) stays per lane.
+  int a_pix[A_PW], a_h0[A_PW], a_w0[A_PW], a_c[A_PW], a_base[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int row = (wid * A_PW + i) * 8 + lr;
@@ -175,6 +176,7 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     } else {
       a_pix[i] = 0; a_h0[i] = -(1 << 20); a_w0[i] = 0;
     }
+    a_base[i] = ((a_pix[i] + a_h0[i] * P.WA + a_w0[i]) * P.CA + a_c[i] * 8) * 2;
   }
   int b_row[B_PW], b_c[B_PW];
 #pragma unroll
@@ -194,13 +196,15 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     if constexpr (C64) {
       const int tap = kt / cb;
       const int chb = (kt - tap * cb) * 64;
-      const int dr = P.tdr[tap], ds = P.tds[tap];
-      const int tbo = (int)P.tb[tap] * P.CA + chb;
+      const int ti = tap / P.tns, tj = tap - ti * P.tns;
+      const int dr = P.dr0 + ti * P.dstep, ds = P.ds0 + tj * P.dstep;
+      const int tbo = ((P.tr0 + ti * P.tstep) * P.S + (P.ts0 + tj * P.tstep)) * P.CA + chb;
+      const int tdelta = ((dr * P.WA + ds) * P.CA + chb) * 2;
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
-        int h = a_h0[i] + dr, w = a_w0[i] + ds;
-        bool ok = (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
-        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + chb + a_c[i] * 8) * 2) : OOB;
+        const int h = a_h0[i] + dr, w = a_w0[i] + ds;
+        const bool ok = (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
+        const uint32_t off = ok ? (uint32_t)(a_base[i] + tdelta) : OOB;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
       }
 #pragma unroll
@@ -278,25 +282,32 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     const int group = tmi * WM + wm;
     const int valid = min(TM * 16, P.M - wrow0);
     if (valid > 0) {
+      const bool full = valid == TM * 16;  // wave-uniform: no per-element masking on full tiles
+      const float inv_valid = 1.f / (float)valid;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         float s[4], q[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float v = 0.f, v2 = 0.f;
+          if (full) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
-            v += a;
-            v2 = fmaf(a, a, v2);
-          }
+            for (int i = 0; i < TM; ++i) {
+              v += acc[i][j][e];
+              v2 = fmaf(acc[i][j][e], acc[i][j][e], v2);
+            }
+          } else {
 #pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            v += __shfl_xor(v, o, 64);
-            v2 += __shfl_xor(v2, o, 64);
+            for (int i = 0; i < TM; ++i) {
+              const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
+              v += a;
+              v2 = fmaf(a, a, v2);
+            }
           }
+          v = row_sum16(v);    // the 16 lanes of a DPP row are the 16 pixels of a tile row
+          v2 = row_sum16(v2);
           s[e] = v;
-          q[e] = fmaxf(v2 - v * v / (float)valid, 0.f);
+          q[e] = fmaxf(v2 - v * v * inv_valid, 0.f);
         }
         const int col = wcol0 + j * 16 + fq * 4;
         if (fr == 0 && col < P.Nout) {
@@ -363,6 +374,7 @@ struct TnArgs {
   FastDiv div_hw, div_w;  // m -> n = m / (Ho*Wo), ho = rem / Wo
   int HoWo, Wo;
   int steps_per_split, nsteps;
+  int accumulate;      // single-split direct store: out += acc instead of out = acc
 };
 
 // LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
@@ -427,47 +439,47 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
     const int sw = (rows[i] & 3) | (((rows[i] >> 3) & 1) << 2);
     chk[i] = lslot ^ (sw << 1);                                 // source chunk for this slot
   }
-  // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel)
-  int a_col[PW], b_dh[PW], b_dw[PW], b_ch[PW];
-  bool b_ok[PW];
+  // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel).
+  // Everything per lane is precomputed; the per-step work is branch-free (selects, no exec
+  // masking): A offset = uniform step base + lane constant, B = one pixel decomposition.
+  int a_lane[PW], b_dh[PW], b_dw[PW], b_chb[PW];
+  bool a_ok[PW], b_ok[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
-    a_col[i] = k0 + chk[i] * 8;
-    if (chk[i] * 8 >= BMG) a_col[i] = P.Kout;  // unused upper half (BMG = 64): force OOB
+    const int acol = k0 + chk[i] * 8;
+    a_ok[i] = chk[i] * 8 < BMG && acol < P.Kout;  // BMG = 64: upper half of the row unused
+    a_lane[i] = (rows[i] * P.Kout + acol) * 2;
     const int col = c0 + chk[i] * 8;
     b_ok[i] = col < P.Ncols;
     const int tap = col / P.C;
-    b_ch[i] = col - tap * P.C;
+    b_chb[i] = (col - tap * P.C) * 2;
     const int r = tap / P.S;
     b_dh[i] = r - P.pad;
     b_dw[i] = (tap - r * P.S) - P.pad;
   }
+  const int WC2 = P.W * P.C * 2, HWC2 = P.H * WC2, C2 = P.C * 2;
 
   auto issue = [&](int step, int buf) {
     char* As = smem + buf * 2 * CFG::TILE_BYTES;
     char* Bs = As + CFG::TILE_BYTES;
     const int mb = step * 64;
+    const int abase = mb * P.Kout * 2;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
-      const int m = mb + rows[i];
-      bool ok = a_col[i] < P.Kout && m < P.Mred;
-      uint32_t off = ok ? (uint32_t)(((int64_t)m * P.Kout + a_col[i]) * 2) : OOB;
-      glds16(rdy, As + (wid * PW + i) * 1024, off);
+      const bool ok = a_ok[i] && (mb + rows[i]) < P.Mred;
+      glds16(rdy, As + (wid * PW + i) * 1024, ok ? (uint32_t)(abase + a_lane[i]) : OOB);
     }
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int m = mb + rows[i];
-      uint32_t off = OOB;
-      if (b_ok[i] && m < P.Mred) {
-        uint32_t n = fdiv((uint32_t)m, P.div_hw);
-        uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
-        uint32_t ho = fdiv(rem, P.div_w);
-        uint32_t wo = rem - ho * (uint32_t)P.Wo;
-        int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride + b_dw[i];
-        if ((unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W)
-          off = (uint32_t)(((((int)n * P.H + h) * P.W + w) * P.C + b_ch[i]) * 2);
-      }
-      glds16(rx, Bs + (wid * PW + i) * 1024, off);
+      const uint32_t n = fdiv((uint32_t)m, P.div_hw);
+      const uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
+      const uint32_t ho = fdiv(rem, P.div_w);
+      const uint32_t wo = rem - ho * (uint32_t)P.Wo;
+      const int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride + b_dw[i];
+      const bool ok = b_ok[i] && m < P.Mred && (unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W;
+      const int off = (int)n * HWC2 + h * WC2 + w * C2 + b_chb[i];
+      glds16(rx, Bs + (wid * PW + i) * 1024, ok ? (uint32_t)off : OOB);
     }
   };
 
@@ -538,6 +550,7 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
         int row = k0 + wm * TM * 16 + i * 16 + fq * 4 + e;
         if (row < P.Kout) {
           if (ATOMIC) unsafeAtomicAdd(o + (int64_t)row * P.Ncols + col, acc[i][j][e]);
+          else if (P.accumulate) o[(int64_t)row * P.Ncols + col] += acc[i][j][e];
           else o[(int64_t)row * P.Ncols + col] = acc[i][j][e];
         }
       }
@@ -545,7 +558,8 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 }
 
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits,
-                                                            int64_t n, float* __restrict__ out) {
+                                                            int64_t n, float* __restrict__ out,
+                                                            int accumulate) {
   int64_t n4 = n / 4;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -554,12 +568,16 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+    if (accumulate) {
+      float4 o = reinterpret_cast<float4*>(out)[i];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
     reinterpret_cast<float4*>(out)[i] = s;
   }
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(int64_t)k * n + i];
-    out[i] = s;
+    out[i] = accumulate ? out[i] + s : s;
   }
 }
 
@@ -628,13 +646,9 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.ash = s.stride; a.asw = s.stride; a.aoff_h = -s.pad; a.aoff_w = -s.pad;
   a.OH = s.Ho; a.OW = s.Wo; a.osh = 1; a.osw = 1; a.oph = 0; a.opw = 0;
   a.dense = 1;
-  a.ntaps = s.R * s.S;
-  if (a.ntaps > MAX_TAPS) throw std::runtime_error("conv_fwd: too many taps");
-  for (int r = 0; r < s.R; ++r)
-    for (int q = 0; q < s.S; ++q) {
-      int i = r * s.S + q;
-      a.tdr[i] = (int8_t)r; a.tds[i] = (int8_t)q; a.tb[i] = (int16_t)i;
-    }
+  a.tnr = s.R; a.tns = s.S; a.ntaps = s.R * s.S;
+  a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
+  a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   bool c64 = (s.C % 64) == 0;
   if (part) {
     if (c64) dispatch_nt<true, true>(a, st, nullptr);
@@ -665,21 +679,14 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
       a.ash = 1; a.asw = 1; a.aoff_h = 0; a.aoff_w = 0;
       a.OH = s.H; a.OW = s.W; a.osh = str; a.osw = str; a.oph = ph; a.opw = pw;
       a.dense = (str == 1);
-      // taps of this parity class: (ph + pad - r) % str == 0 -> ho = i + (ph + pad - r)/str
-      int nt = 0;
-      for (int r = 0; r < s.R; ++r) {
-        int dh = ph + s.pad - r;
-        if (((dh % str) + str) % str != 0) continue;
-        for (int q = 0; q < s.S; ++q) {
-          int dw = pw + s.pad - q;
-          if (((dw % str) + str) % str != 0) continue;
-          a.tdr[nt] = (int8_t)(dh >= 0 ? dh / str : -((-dh) / str));
-          a.tds[nt] = (int8_t)(dw >= 0 ? dw / str : -((-dw) / str));
-          a.tb[nt] = (int16_t)(r * s.S + q);
-          ++nt;
-        }
-      }
-      a.ntaps = nt;  // nt == 0 -> kernel writes zeros for this class
+      // taps of this parity class: r = r0 + str*i with (ph + pad - r0) % str == 0, and the
+      // dy row it reads is ho = hi + (ph + pad - r)/str = hi + dr0 - i
+      const int r0 = (ph + s.pad) % str, s0 = (pw + s.pad) % str;
+      a.tnr = r0 < s.R ? (s.R - r0 + str - 1) / str : 0;
+      a.tns = s0 < s.S ? (s.S - s0 + str - 1) / str : 0;
+      a.ntaps = a.tnr * a.tns;  // 0 -> kernel writes zeros for this class
+      a.tr0 = r0; a.ts0 = s0; a.tstep = str;
+      a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;
       dispatch_nt<true, false>(a, st, nullptr);
     }
 }
@@ -731,7 +738,7 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
 }
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, bool deterministic, hipStream_t st) {
+                       const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st) {
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
   WgradPlan p = plan_wgrad(s, deterministic);
   const bool slab = deterministic && p.splits > 1;
@@ -748,8 +755,9 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.div_w = make_fastdiv((uint32_t)s.Wo);
   a.steps_per_split = p.steps_per_split;
   a.nsteps = p.nsteps;
+  a.accumulate = accumulate ? 1 : 0;
   const int64_t n = (int64_t)s.K * a.Ncols;
-  if (atomic) hipMemsetAsync(dw, 0, n * sizeof(float), st);
+  if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   if (p.bmg == 64) {
     if (atomic) run_tn<64, 128, true>(a, p.tiles, p.splits, st);
     else run_tn<64, 128, false>(a, p.tiles, p.splits, st);
@@ -760,7 +768,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   if (slab) {
     int64_t b = (n / 4 + 255) / 256;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 4096))),
-                       dim3(256), 0, st, ws, p.splits, n, dw);
+                       dim3(256), 0, st, ws, p.splits, n, dw, accumulate ? 1 : 0);
     check_launch("splitk_reduce");
   }
 }

@@ -37,8 +37,10 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
+// accumulate: dw += wgrad (autograd accumulation semantics; lets the block write straight into
+// the flat gradient buffer), else dw = wgrad.
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, bool deterministic, hipStream_t st);
+                       const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st);
 
 // -------------------------------------------------------------- bn_act.hip
 // part[ngroups][2][K] (group g has min(grows, M-grows*g) rows) -> out[4][K] = mean, invstd,
@@ -54,17 +56,21 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
                        hipStream_t st);
-// sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * (z>0 if relu); ws >= bn_bwd_ws_floats
+// Backward BN.  stats = bn_finalize output [4][K] (mean, invstd, scale, shift).  mask: 0 = no
+// ReLU, 1 = ReLU mask from z (> 0), 2 = ReLU mask recomputed from y (y*scale + shift > 0).
+// sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * mask; ws >= bn_bwd_ws_floats(M, K)
 size_t bn_bwd_ws_floats(int64_t M, int K);
+// If dgamma/dbeta are non-null the final stage also accumulates dgamma += sum_gx*invstd and
+// dbeta += sum_g into them (parameter gradients written in place).
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
-                              const float* mean, bool relu, int64_t M, int K, float* ws,
-                              float* sums, hipStream_t st);
-// dy = gamma*invstd*(g - sum_g/M - xhat*sum_gx*invstd/M) (training) / gamma*invstd*g (eval);
+                              const float* stats, int mask, int64_t M, int K, float* ws,
+                              float* sums, float* dgamma, float* dbeta, hipStream_t st);
+// dy = gamma*invstd*(g - sum_g/M - (y-mean)*sum_gx*invstd^2/M) (training) or gamma*invstd*g;
 // dres = g (if non-null)
 void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
-                             const float* mean, const float* invstd, const float* gamma,
-                             const float* sums, bool relu, bool training, int64_t M, int K,
-                             uint16_t* dy, uint16_t* dres, hipStream_t st);
+                             const float* stats, const float* gamma, const float* sums, int mask,
+                             bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
+                             hipStream_t st);
 
 // ---------------------------------------------------------------- pool.hip
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,

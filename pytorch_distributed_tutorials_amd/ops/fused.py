@@ -83,23 +83,27 @@ class _ConvBN(torch.autograd.Function):
                 mean, var = running_mean.float(), running_var.float()
             invstd = torch.rsqrt(var + eps)
             z = ref.bn_act_fwd(y, mean, invstd, gamma, beta, residual, relu, x.dtype)
-        ctx.save_for_backward(x, weight, wk, y, z, mean, invstd, gamma)
+            sc = gamma.float() * invstd
+            stats = torch.stack([mean, invstd, sc, beta.float() - mean * sc])
+        ctx.save_for_backward(x, weight, y, z, stats, gamma)
         ctx.cfg = (stride, pad, relu, training, residual is not None)
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        x, weight, wk, y, z, mean, invstd, gamma = ctx.saved_tensors
+        x, weight, y, z, stats, gamma = ctx.saved_tensors
+        mean, invstd = stats[0], stats[1]
         stride, pad, relu, training, has_res = ctx.cfg
         dz = dz.contiguous()
         need_x = ctx.needs_input_grad[0]
         need_w = ctx.needs_input_grad[1]
         if dz.is_cuda:
             C = native()
-            sums = C.bn_act_bwd_reduce(dz, z, y, mean, relu)     # [sum g, sum g*(y-mean)]
+            # ReLU mask: from z when a residual was added, else recomputed from y (no z read)
+            mask = (1 if has_res else 2) if relu else 0
+            sums = C.bn_act_bwd_reduce(dz, z, y, stats, mask)    # [sum g, sum g*(y-mean)]
             dbeta, dgamma = sums[0], sums[1] * invstd
-            dy, dres = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sums,
-                                          relu, training, has_res)
+            dy, dres = C.bn_act_bwd_apply(dz, z, y, stats, gamma, sums, mask, training, has_res)
             dx = C.conv_dgrad(dy, weight, list(x.shape), stride, pad) if need_x else None
             dw = C.conv_wgrad(dy, x, list(weight.shape), stride, pad, deterministic()) \
                 if need_w else None
@@ -258,9 +262,8 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:
         stats = C.bn_eval_params(rm, rv, gamma, beta, float(eps))
-    mean, invstd, scale, shift = stats.unbind(0)
-    z = C.bn_act_fwd(y, scale, shift, residual, relu)
-    return z, y, mean, invstd
+    z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu)
+    return z, y, stats
 
 
 class _ResidualBlock(torch.autograd.Function):
@@ -284,7 +287,7 @@ class _ResidualBlock(torch.autograd.Function):
         if ds_cfg is not None:
             w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
             st, pd, tr, mo, ep = ds_cfg
-            res, y_ds, mu_ds, is_ds = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None)
+            res, y_ds, st_ds = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None)
         else:
             res = x
         h = x
@@ -292,15 +295,16 @@ class _ResidualBlock(torch.autograd.Function):
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
             last = i == nch - 1
-            z, y, mu, istd = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
-                                       res if last else None)
-            outs.append((z, y, mu, istd))
+            z, y, stt = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
+                                  res if last else None)
+            outs.append((z, y, stt))
             h = z
-        for z, y, mu, istd in outs:
-            saved += [z, y, mu, istd]
+        for z, y, stt in outs:
+            saved += [z, y, stt]
         if ds_cfg is not None:
-            saved += [y_ds, mu_ds, is_ds]
+            saved += [y_ds, st_ds]
         ctx.save_for_backward(*saved, *tensors)
+        ctx.params = tensors  # the Parameter objects: gradients may be written into flat views
         ctx.spec = spec
         ctx.ntensors = len(tensors)
         return h
@@ -312,27 +316,48 @@ class _ResidualBlock(torch.autograd.Function):
         nch = len(chain)
         sv = ctx.saved_tensors
         x = sv[0]
-        units = [sv[1 + 4 * i:5 + 4 * i] for i in range(nch)]
-        pos = 1 + 4 * nch
+        units = [sv[1 + 3 * i:4 + 3 * i] for i in range(nch)]
+        pos = 1 + 3 * nch
         if ds_cfg is not None:
-            y_ds, mu_ds, is_ds = sv[pos:pos + 3]
-            pos += 3
+            y_ds, st_ds = sv[pos:pos + 2]
+            pos += 2
         tensors = sv[pos:]
         grads = [None] * ctx.ntensors
         dz = dz.contiguous()
         det = deterministic()
         g_short = None
+        params = ctx.params
+        sunk = []  # parameters whose gradient was accumulated in place into the flat buffer
+
+        def wgrad(j, dy_, xin_, st_, pd_):
+            w_ = tensors[j]
+            sink = _grad_sink(params[j])
+            if sink is not None:
+                C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det, sink)
+                sunk.append(params[j])
+            else:
+                grads[j] = C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det).to(w_.dtype)
+
+        def bnreduce(j, dz_, z_, y_, stt_, mask_):
+            sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
+            if sg is not None and sb is not None:
+                sums_ = C.bn_act_bwd_reduce(dz_, z_, y_, stt_, mask_, sg, sb)
+                sunk.extend([params[j + 1], params[j + 2]])
+            else:
+                sums_ = C.bn_act_bwd_reduce(dz_, z_, y_, stt_, mask_)
+                grads[j + 1] = sums_[1] * stt_[1]
+                grads[j + 2] = sums_[0]
+            return sums_
         for i in reversed(range(nch)):
             st, pd, tr, mo, ep = chain[i]
-            z, y, mu, istd = units[i]
+            z, y, stt = units[i]
             w, gamma = tensors[5 * i], tensors[5 * i + 1]
             xin = x if i == 0 else units[i - 1][0]
             last = i == nch - 1
-            sums = C.bn_act_bwd_reduce(dz, z, y, mu, True)
-            dy, dres = C.bn_act_bwd_apply(dz, z, y, mu, istd, gamma, sums, True, tr, last)
-            grads[5 * i + 1] = sums[1] * istd
-            grads[5 * i + 2] = sums[0]
-            grads[5 * i] = C.conv_wgrad(dy, xin, list(w.shape), st, pd, det).to(w.dtype)
+            mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
+            sums = bnreduce(5 * i, dz, z, y, stt, mask)
+            dy, dres = C.bn_act_bwd_apply(dz, z, y, stt, gamma, sums, mask, tr, last)
+            wgrad(5 * i, dy, xin, st, pd)
             if last:
                 g_short = dres
             if i > 0:
@@ -342,17 +367,25 @@ class _ResidualBlock(torch.autograd.Function):
                 if ds_cfg is not None:
                     st2, pd2, tr2, _, _ = ds_cfg
                     wds, gds = tensors[5 * nch], tensors[5 * nch + 1]
-                    sums_ds = C.bn_act_bwd_reduce(g_short, g_short, y_ds, mu_ds, False)
-                    dy_ds, _ = C.bn_act_bwd_apply(g_short, g_short, y_ds, mu_ds, is_ds, gds, sums_ds,
-                                                  False, tr2, False)
-                    grads[5 * nch + 1] = sums_ds[1] * is_ds
-                    grads[5 * nch + 2] = sums_ds[0]
-                    grads[5 * nch] = C.conv_wgrad(dy_ds, x, list(wds.shape), st2, pd2, det).to(wds.dtype)
+                    sums_ds = bnreduce(5 * nch, g_short, g_short, y_ds, st_ds, 0)
+                    dy_ds, _ = C.bn_act_bwd_apply(g_short, g_short, y_ds, st_ds, gds, sums_ds,
+                                                  0, tr2, False)
+                    wgrad(5 * nch, dy_ds, x, st2, pd2)
                     addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2)
                 else:
                     addend = g_short
                 dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend) if ctx.needs_input_grad[0] else None
+        if sunk:
+            sunk[0]._pdt_flat.mark_ready(sunk)
         return (dz, None, *grads)
+
+
+def _grad_sink(p):
+    """Flat-buffer gradient view to accumulate into, if the parameter lives in a FlatParamSpace."""
+    sp = getattr(p, "_pdt_flat", None)
+    if sp is None or not p.requires_grad or not p.is_cuda:
+        return None
+    return sp.grad_sink(p)
 
 
 def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:

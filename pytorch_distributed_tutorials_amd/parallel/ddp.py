@@ -69,6 +69,15 @@ class _PyReducer:
         self.next = 0
         self.order = []
 
+    def mark_ready_external(self, idx):
+        for i in idx:
+            if not (self.enabled and self._expect):
+                return
+            if not self._queued:
+                self._queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._final)
+            self._mark(i, False)
+
     def prepare_for_backward(self):
         self._reset()
         self._expect = self.enabled
@@ -200,6 +209,7 @@ class DistributedDataParallel(nn.Module):
                 self.reducer = _PyReducer(sp.params, sp.grad_views, bucket_of, flats,
                                           self._py_launch, self._py_finalize)
             self._flats = flats
+            self.space.reducer = self.reducer
 
     # ------------------------------------------------------------- helpers
     def _verify_params_across_processes(self, params) -> None:

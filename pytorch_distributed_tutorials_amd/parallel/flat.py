@@ -45,6 +45,8 @@ class FlatParamSpace:
         self.param_flat = torch.empty(off, device=dev, dtype=dt)
         self.grad_flat = torch.zeros(off, device=dev, dtype=dt)
         self.grad_views: List[torch.Tensor] = []
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.reducer = None  # set by DistributedDataParallel when gradients are all-reduced
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 view = torch.as_strided(self.param_flat, p.shape, p.stride(), o)
@@ -72,6 +74,25 @@ class FlatParamSpace:
                     if p.grad.data_ptr() != g.data_ptr():
                         g.copy_(p.grad)
                 p.grad = g
+
+    def grad_sink(self, p: torch.nn.Parameter) -> torch.Tensor:
+        """The flat view ``p.grad`` must live in, ready for a kernel to ACCUMULATE into
+        (autograd semantics).  Used by fused native backward passes that write parameter
+        gradients in place instead of returning them to autograd."""
+        g = self.grad_views[self.index[id(p)]]
+        if p.grad is not g:
+            with torch.no_grad():
+                if p.grad is None:
+                    g.zero_()
+                elif p.grad.data_ptr() != g.data_ptr():
+                    g.copy_(p.grad)
+            p.grad = g
+        return g
+
+    def mark_ready(self, params) -> None:
+        """Tell the reducer that these parameters' gradients are final in their views."""
+        if self.reducer is not None:
+            self.reducer.mark_ready_external([self.index[id(p)] for p in params])
 
     def zero_grad(self) -> None:
         self.grad_flat.zero_()

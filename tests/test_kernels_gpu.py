@@ -137,15 +137,18 @@ def test_bn_act_fwd_bwd(gpu, native_ext, relu, res):
     z = C.bn_act_fwd(y, scale, shift, r, relu)
     zr = ref.bn_act_fwd(y, mean, invstd, gamma, beta, r, relu, torch.float32)
     assert (z.float() - zr).abs().max().item() < 3e-2
+    stats = torch.stack([mean, invstd, scale, shift]).contiguous()
     dz = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
-    sums = C.bn_act_bwd_reduce(dz, z, y, mean, relu)
-    dy, dres = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sums, relu, True, res)
     dyr, dgr, dbr, dresr = ref.bn_act_bwd(dz, z, y, mean, invstd, gamma, relu, True, res, torch.float32)
-    assert torch.allclose(sums[0], dbr, rtol=1e-3, atol=1e-2)
-    assert torch.allclose(sums[1] * invstd, dgr, rtol=1e-3, atol=1e-2)
-    assert _rel_err(dy, dyr) < 1e-2
-    if res:
-        assert _rel_err(dres, dresr) < 1e-2
+    modes = ([1, 2] if not res else [1]) if relu else [0]
+    for mask in modes:  # 1: mask from z, 2: mask recomputed from y (must agree)
+        sums = C.bn_act_bwd_reduce(dz, z, y, stats, mask)
+        dy, dres = C.bn_act_bwd_apply(dz, z, y, stats, gamma, sums, mask, True, res)
+        assert torch.allclose(sums[0], dbr, rtol=1e-3, atol=1e-2)
+        assert torch.allclose(sums[1] * invstd, dgr, rtol=1e-3, atol=1e-2)
+        assert _rel_err(dy, dyr) < 1e-2
+        if res:
+            assert _rel_err(dres, dresr) < 1e-2
 
 
 def test_bn_against_torch_batchnorm(gpu, native_ext):
@@ -165,8 +168,10 @@ def test_bn_against_torch_batchnorm(gpu, native_ext):
     z = C.bn_act_fwd(y, gamma.detach() * invstd, beta.detach() - mean * gamma.detach() * invstd, None, True)
     assert _rel_err(z.permute(0, 3, 1, 2), out) < 1e-2
     dz = gout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    sums = C.bn_act_bwd_reduce(dz, z, y, mean, True)
-    dy, _ = C.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma.detach(), sums, True, True, False)
+    sc = gamma.detach() * invstd
+    stats = torch.stack([mean, invstd, sc, beta.detach() - mean * sc]).contiguous()
+    sums = C.bn_act_bwd_reduce(dz, z, y, stats, 2)
+    dy, _ = C.bn_act_bwd_apply(dz, z, y, stats, gamma.detach(), sums, 2, True, False)
     assert _rel_err(dy.permute(0, 3, 1, 2), xb.grad) < 3e-2
     assert _rel_err(sums[1] * invstd, gamma.grad) < 3e-2
     assert _rel_err(sums[0], beta.grad) < 3e-2
@@ -293,3 +298,31 @@ def test_residual_block_matches_unit_path(gpu, native_ext, arch, idx):
         assert _rel_err(p1.grad, p2.grad) < 1e-2, n1
     for b1, b2 in zip(blk.buffers(), blk2.buffers()):
         assert torch.equal(b1, b2)
+
+
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_inplace_grad_sinks_match_autograd(gpu, native_ext, deterministic):
+    """Block backward writing weight/BN grads straight into the flat buffer (DDP flat space) must
+    equal the autograd-returned gradients, including accumulation over two backward passes."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_tutorials_amd.utils import seed as seedmod
+    old = seedmod._DETERMINISTIC
+    seedmod._DETERMINISTIC = deterministic
+    try:
+        torch.manual_seed(0)
+        m1 = build_model("resnet50", num_classes=10).to(gpu).set_impl("native")
+        m2 = copy.deepcopy(m1)
+        ddp = DistributedDataParallel(m2)   # world 1: flat space, grads sunk in place
+        x = torch.randn(2, 3, 64, 64, device=gpu)
+        y = torch.randint(0, 10, (2,), device=gpu)
+        for _ in range(2):  # no zero_grad in between: gradients must accumulate
+            ops.cross_entropy(m1(x), y).backward()
+            ops.cross_entropy(ddp(x), y).backward()
+        for (n1, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+            assert p2.grad is not None, n1
+            assert _rel_err(p2.grad, p1.grad) < 2e-2, n1
+    finally:
+        seedmod._DETERMINISTIC = old
