@@ -397,32 +397,59 @@ __device__ __forceinline__ v4i cat_frag(v4s_t lo, v4s_t hi) {
   return __builtin_bit_cast(v4i, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// 128-B-row variant for the [64 m][64 kout] A tile of a BMG = 64 wgrad: swizzle
+// sw(m) = ((m>>1)&1) | ((m>>3)&1)<<1 applied as chunk ^ (sw<<1) keeps each tr-read chunk pair
+// together; a half-wave's rows {m..m+3, m+8..m+11} land in 8 distinct 32-B bank windows
+// ((m&1)*4 + (pair ^ sw)), so the 128-B image is conflict-free too and the tile DMA moves only
+// the bytes the MFMAs consume (the 256-B image fetched a never-read upper half).
+__device__ __forceinline__ int swz128_tr(int row, int chunk) {
+  int sw = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return row * 128 + ((chunk ^ (sw << 1)) << 4);
+}
+
+template <int ROWB>
+__device__ __forceinline__ int swz_img(int row, int chunk) {
+  if constexpr (ROWB == 256) return swz256(row, chunk);
+  else return swz128_tr(row, chunk);
+}
+
 template <int BMG, int BNG>
 struct TnCfg {
+  static_assert(BNG == 128 && (BMG == 64 || BMG == 128), "TN tile shapes");
   static constexpr int NT = 256;
-  static constexpr int TILE_BYTES = 64 * 256;        // one [64 m][<=128 col] tile, 256-B pitch
-  static constexpr int SMEM = 2 * 2 * TILE_BYTES;    // 2 buffers x (A, B)
-  static constexpr int TM = BMG / 2 / 16;            // 2x2 waves
+  static constexpr int A_ROWB = BMG * 2;              // bytes per m row of the dy tile image
+  static constexpr int A_BYTES = 64 * A_ROWB;
+  static constexpr int B_BYTES = 64 * 256;            // [64 m][128 col], 256-B rows
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int SMEM = 2 * STAGE;              // 2 pipeline buffers
+  static constexpr int TM = BMG / 2 / 16;             // 2x2 waves
   static constexpr int TN = BNG / 2 / 16;
-  static constexpr int PW = 16 / 4;                  // 1-KiB DMA instructions per wave per tile
+  static constexpr int A_LPR = A_ROWB / 16;           // lanes per row in one 1-KiB DMA instruction
+  static constexpr int A_RPI = 64 / A_LPR;            // rows per instruction
+  static constexpr int A_PW = A_BYTES / 1024 / 4;     // DMA instructions per wave per tile
+  static constexpr int B_PW = B_BYTES / 1024 / 4;
 };
 
-// Main loop as igemm_nt (LDS-DMA, source-side swizzle, 2 buffers, one barrier per K-step).  A DMA
-// wave instruction covers 4 rows (m) x 256 B; lane l fetches row 4g + (l>>4), slot l&15 holding
-// chunk (l&15) ^ (swz(m)<<1).  With BMG = 64 the upper half of each 256-B row is fetched but never
-// read (keeps the one image layout for both tile widths).
+// Main loop as igemm_nt (LDS-DMA, source-side swizzle, 2 buffers, one barrier per K-step).  One
+// DMA wave instruction moves 1 KiB = A_RPI rows of the tile; lane l fetches row
+// A_RPI*g + l/A_LPR, LDS slot l%A_LPR holding the source chunk slot ^ (swz(m)<<1).
+// Grid: 1-D over (split, tile) with split-major logical ids after the XCD remap, so the
+// column tiles of one split -- which read the same dy rows and overlapping x rows -- run on
+// the same XCD and share its L2.
 template <int BMG, int BNG, bool ATOMIC>
 __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   using CFG = TnCfg<BMG, BNG>;
-  constexpr int TM = CFG::TM, TN = CFG::TN, PW = CFG::PW;
+  constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Ncols + BNG - 1) / BNG;
   const int ntm = (P.Kout + BMG - 1) / BMG;
-  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tiles = ntm * ntn;
+  const int lid = xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int split = lid / tiles;
+  const int bid = lid - split * tiles;
   const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
   const int k0 = tmi * BMG, c0 = tni * BNG;
-  const int split = blockIdx.y;
   const int s_begin = split * P.steps_per_split;
   const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
 
@@ -431,25 +458,27 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
 
-  const int lrow = lane >> 4, lslot = lane & 15;
-  int rows[PW], chk[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    rows[i] = (wid * PW + i) * 4 + lrow;                       // m row within the 64-row tile
-    const int sw = (rows[i] & 3) | (((rows[i] >> 3) & 1) << 2);
-    chk[i] = lslot ^ (sw << 1);                                 // source chunk for this slot
-  }
   // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel).
   // Everything per lane is precomputed; the per-step work is branch-free (selects, no exec
   // masking): A offset = uniform step base + lane constant, B = one pixel decomposition.
-  int a_lane[PW], b_dh[PW], b_dw[PW], b_chb[PW];
-  bool a_ok[PW], b_ok[PW];
+  int arow[A_PW], a_lane[A_PW];
+  bool a_ok[A_PW];
 #pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int acol = k0 + chk[i] * 8;
-    a_ok[i] = chk[i] * 8 < BMG && acol < P.Kout;  // BMG = 64: upper half of the row unused
-    a_lane[i] = (rows[i] * P.Kout + acol) * 2;
-    const int col = c0 + chk[i] * 8;
+  for (int i = 0; i < A_PW; ++i) {
+    arow[i] = (wid * A_PW + i) * CFG::A_RPI + lane / CFG::A_LPR;
+    const int slot = lane % CFG::A_LPR;
+    const int chk = (swz_img<CFG::A_ROWB>(arow[i], slot) - arow[i] * CFG::A_ROWB) >> 4;  // involution
+    const int acol = k0 + chk * 8;
+    a_ok[i] = acol < P.Kout;
+    a_lane[i] = (arow[i] * P.Kout + acol) * 2;
+  }
+  int brow[B_PW], b_dh[B_PW], b_dw[B_PW], b_chb[B_PW];
+  bool b_ok[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    brow[i] = (wid * B_PW + i) * 4 + (lane >> 4);
+    const int chk = (swz256(brow[i], lane & 15) - brow[i] * 256) >> 4;
+    const int col = c0 + chk * 8;
     b_ok[i] = col < P.Ncols;
     const int tap = col / P.C;
     b_chb[i] = (col - tap * P.C) * 2;
@@ -460,18 +489,18 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   const int WC2 = P.W * P.C * 2, HWC2 = P.H * WC2, C2 = P.C * 2;
 
   auto issue = [&](int step, int buf) {
-    char* As = smem + buf * 2 * CFG::TILE_BYTES;
-    char* Bs = As + CFG::TILE_BYTES;
+    char* As = smem + buf * CFG::STAGE;
+    char* Bs = As + CFG::A_BYTES;
     const int mb = step * 64;
     const int abase = mb * P.Kout * 2;
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const bool ok = a_ok[i] && (mb + rows[i]) < P.Mred;
-      glds16(rdy, As + (wid * PW + i) * 1024, ok ? (uint32_t)(abase + a_lane[i]) : OOB);
+    for (int i = 0; i < A_PW; ++i) {
+      const bool ok = a_ok[i] && (mb + arow[i]) < P.Mred;
+      glds16(rdy, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(abase + a_lane[i]) : OOB);
     }
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int m = mb + rows[i];
+    for (int i = 0; i < B_PW; ++i) {
+      const int m = mb + brow[i];
       const uint32_t n = fdiv((uint32_t)m, P.div_hw);
       const uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
       const uint32_t ho = fdiv(rem, P.div_w);
@@ -479,7 +508,7 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
       const int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride + b_dw[i];
       const bool ok = b_ok[i] && m < P.Mred && (unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W;
       const int off = (int)n * HWC2 + h * WC2 + w * C2 + b_chb[i];
-      glds16(rx, Bs + (wid * PW + i) * 1024, ok ? (uint32_t)off : OOB);
+      glds16(rx, Bs + (wid * B_PW + i) * 1024, ok ? (uint32_t)off : OOB);
     }
   };
 
@@ -494,8 +523,11 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  auto frag_addr = [&](const char* base, int row, int col) -> const char* {
-    // col multiple of 4; chunk = col/8, byte-in-chunk = (col%8)*2
+  // col multiple of 4; chunk = col/8, byte-in-chunk = (col%8)*2
+  auto frag_a = [&](const char* base, int row, int col) -> const char* {
+    return base + swz_img<CFG::A_ROWB>(row, col >> 3) + ((col & 7) << 1);
+  };
+  auto frag_b = [&](const char* base, int row, int col) -> const char* {
     return base + swz256(row, col >> 3) + ((col & 7) << 1);
   };
 
@@ -505,8 +537,8 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
   for (int step = s_begin; step < s_end; ++step) {
     const int cur = (step - s_begin) & 1;
     if (step + 1 < s_end) issue(step + 1, cur ^ 1);
-    const char* As = smem + cur * 2 * CFG::TILE_BYTES;
-    const char* Bs = As + CFG::TILE_BYTES;
+    const char* As = smem + cur * CFG::STAGE;
+    const char* Bs = As + CFG::A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int rowA = ks * 32 + 8 * g + tq;  // m row of the first tr block
@@ -514,15 +546,15 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         int col = wm * TM * 16 + i * 16 + 4 * tp;
-        v4s_t lo = ds_read_tr(frag_addr(As, rowA, col));
-        v4s_t hi = ds_read_tr(frag_addr(As, rowA + 4, col));
+        v4s_t lo = ds_read_tr(frag_a(As, rowA, col));
+        v4s_t hi = ds_read_tr(frag_a(As, rowA + 4, col));
         af[i] = cat_frag(lo, hi);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         int col = wn * TN * 16 + j * 16 + 4 * tp;
-        v4s_t lo = ds_read_tr(frag_addr(Bs, rowA, col));
-        v4s_t hi = ds_read_tr(frag_addr(Bs, rowA + 4, col));
+        v4s_t lo = ds_read_tr(frag_b(Bs, rowA, col));
+        v4s_t hi = ds_read_tr(frag_b(Bs, rowA + 4, col));
         bfr[j] = cat_frag(lo, hi);
       }
 #pragma unroll
@@ -733,7 +765,7 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(tiles, splits), dim3(256), CFG::SMEM, st, a);
+  hipLaunchKernelGGL(kfn, dim3(tiles * splits), dim3(256), CFG::SMEM, st, a);
   check_launch("igemm_tn");
 }
 
