@@ -10,7 +10,11 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <optional>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
 
 #include "comm/rccl_comm.h"
 #include "ddp/reducer.h"
@@ -20,6 +24,37 @@ namespace py = pybind11;
 using at::Tensor;
 
 namespace {
+
+// ---------------------------------------------------------------- debug mode
+// PDT_SYNC_CHECK=1 (or _C.set_sync_check(True)): every op synchronizes the device after its
+// launches and turns an asynchronous kernel fault into an exception naming the op that caused
+// it (the role CUDA_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL play, scoped to this extension).
+bool g_sync_check = [] {
+  const char* e = std::getenv("PDT_SYNC_CHECK");
+  return e && e[0] == '1';
+}();
+
+void sync_check(const char* op) {
+  if (!g_sync_check) return;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("PDT_SYNC_CHECK: ") + op + ": " + hipGetErrorString(e));
+}
+
+template <typename R, typename... A>
+auto checked(const char* op, R (*f)(A...)) {
+  return [op, f](A... a) -> R {
+    if constexpr (std::is_void_v<R>) {
+      f(std::forward<A>(a)...);
+      sync_check(op);
+    } else {
+      R r = f(std::forward<A>(a)...);
+      sync_check(op);
+      return r;
+    }
+  };
+}
 
 hipStream_t cur_stream(const Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.get_device()).stream();
@@ -126,6 +161,65 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
   }
   pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, cur_stream(dy));
   return dx;
+}
+
+// dgrad with the BatchNorm backward of the unit that produced x fused into the epilogue:
+// returns (g, sums) with g = dx * relu'(unit) (mask 0/1/2 as bn_act_bwd_reduce) and
+// sums[2][C] = (sum g, sum g*(y - mean)); optional dgamma/dbeta accumulate like
+// bn_act_bwd_reduce.  bn_act_bwd_apply(g, ..., mask=0) then yields that unit's dy.
+std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs,
+                                         int64_t stride, int64_t pad,
+                                         const std::optional<Tensor>& addend, const Tensor& y,
+                                         const std::optional<Tensor>& z, const Tensor& stats,
+                                         int64_t mask, const std::optional<Tensor>& dgamma,
+                                         const std::optional<Tensor>& dbeta) {
+  check_bf16_nhwc(dy, "dy");
+  check_bf16_nhwc(y, "y");
+  TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
+  TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
+  c10::hip::HIPGuard g(dy.get_device());
+  auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
+  TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
+  TORCH_CHECK(y.size(0) == s.N && y.size(1) == s.H && y.size(2) == s.W && y.size(3) == s.C,
+              "dgrad_bn: y must have the shape of x");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * s.C && stats.is_contiguous(),
+              "stats must be fp32 [4, C]");
+  TORCH_CHECK(mask >= 0 && mask <= 2, "mask must be 0, 1 or 2");
+  const uint16_t* zp = nullptr;
+  if (mask == 1) {
+    TORCH_CHECK(z.has_value() && z->defined(), "mask 1 needs z");
+    check_bf16_nhwc(*z, "z");
+    TORCH_CHECK(z->sizes() == y.sizes(), "z shape mismatch");
+    zp = cbf(*z);
+  }
+  Tensor wt = pack_weight_t(w);
+  auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
+  const uint16_t* ap = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16_nhwc(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    ap = cbf(*addend);
+  }
+  const int G = pdt::conv_dgrad_bn_groups(s);
+  auto fopt = dy.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)G * 2 * s.C}, fopt);
+  auto ws = at::empty({(int64_t)pdt::bn_bwd_part_ws_floats(G, s.C)}, fopt);
+  auto sums = at::empty({2, s.C}, fopt);
+  pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
+  hipStream_t st = cur_stream(dy);
+  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, st, &bn);
+  float* dg = nullptr;
+  float* db = nullptr;
+  if (dgamma.has_value() && dgamma->defined()) {
+    TORCH_CHECK(dbeta.has_value() && dbeta->defined(), "dgamma and dbeta go together");
+    TORCH_CHECK(dgamma->is_contiguous() && dbeta->is_contiguous() && dgamma->numel() == s.C &&
+                dbeta->numel() == s.C && dgamma->scalar_type() == at::kFloat, "dgamma/dbeta: fp32 [C]");
+    dg = dgamma->data_ptr<float>();
+    db = dbeta->data_ptr<float>();
+  }
+  pdt::launch_bn_bwd_part_reduce(part.data_ptr<float>(), G, s.C, ws.data_ptr<float>(),
+                                 sums.data_ptr<float>(), stats.data_ptr<float>() + s.C, dg, db, st);
+  return {dx, sums};
 }
 
 // dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
@@ -353,30 +447,36 @@ void sgd_step(Tensor p, const Tensor& g, Tensor buf, double lr, double momentum,
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) native kernels, RCCL communicator and DDP reducer";
-  m.def("image_to_nhwc", &image_to_nhwc);
-  m.def("pack_weight", &pack_weight, py::arg("w"), py::arg("cpad") = 0);
-  m.def("pack_weight_t", &pack_weight_t);
-  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
+  m.def("image_to_nhwc", checked("image_to_nhwc", &image_to_nhwc));
+  m.def("pack_weight", checked("pack_weight", &pack_weight), py::arg("w"), py::arg("cpad") = 0);
+  m.def("pack_weight_t", checked("pack_weight_t", &pack_weight_t));
+  m.def("conv_fwd", checked("conv_fwd", &conv_fwd), py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("stats"));
-  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"), py::arg("stride"),
+  m.def("conv_dgrad", checked("conv_dgrad", &conv_dgrad), py::arg("dy"), py::arg("w"), py::arg("x_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("addend") = py::none());
-  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
+  m.def("conv_dgrad_bn", checked("conv_dgrad_bn", &conv_dgrad_bn), py::arg("dy"), py::arg("w"),
+        py::arg("x_shape"), py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("y"),
+        py::arg("z"), py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
+  m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
-  m.def("bn_finalize", &bn_finalize);
-  m.def("bn_eval_params", &bn_eval_params);
-  m.def("bn_act_fwd", &bn_act_fwd, py::arg("y"), py::arg("scale"), py::arg("shift"),
+  m.def("bn_finalize", checked("bn_finalize", &bn_finalize));
+  m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
+  m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"));
-  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("y"),
+  m.def("bn_act_bwd_reduce", checked("bn_act_bwd_reduce", &bn_act_bwd_reduce), py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
-  m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
-  m.def("maxpool_fwd", &maxpool_fwd);
-  m.def("maxpool_bwd", &maxpool_bwd);
-  m.def("avgpool_fwd", &avgpool_fwd);
-  m.def("avgpool_bwd", &avgpool_bwd);
-  m.def("softmax_xent", &softmax_xent);
-  m.def("top1_correct", &top1_correct);
-  m.def("sgd_step", &sgd_step);
+  m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply));
+  m.def("maxpool_fwd", checked("maxpool_fwd", &maxpool_fwd));
+  m.def("maxpool_bwd", checked("maxpool_bwd", &maxpool_bwd));
+  m.def("avgpool_fwd", checked("avgpool_fwd", &avgpool_fwd));
+  m.def("avgpool_bwd", checked("avgpool_bwd", &avgpool_bwd));
+  m.def("softmax_xent", checked("softmax_xent", &softmax_xent));
+  m.def("top1_correct", checked("top1_correct", &top1_correct));
+  m.def("sgd_step", checked("sgd_step", &sgd_step));
   m.def("conv_fwd_group_rows", &pdt::conv_fwd_group_rows);
+  m.def("set_sync_check", [](bool on) { g_sync_check = on; });
+  m.def("sync_check_enabled", []() { return g_sync_check; });
 
   py::class_<pdt::RcclComm, std::shared_ptr<pdt::RcclComm>>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(pdt::RcclComm::unique_id()); })
@@ -416,5 +516,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("enabled", &pdt::Reducer::enabled)
       .def_property_readonly("num_buckets", &pdt::Reducer::num_buckets)
       .def_property_readonly("iterations", &pdt::Reducer::iterations)
-      .def("last_launch_order", &pdt::Reducer::last_launch_order);
+      .def("last_launch_order", &pdt::Reducer::last_launch_order)
+      .def("set_timing", &pdt::Reducer::set_timing)
+      .def("comm_timing", &pdt::Reducer::comm_timing, py::call_guard<py::gil_scoped_release>())
+      .def("set_strict", &pdt::Reducer::set_strict)
+      .def_property_readonly("duplicate_marks", &pdt::Reducer::duplicate_marks);
 }

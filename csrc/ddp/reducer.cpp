@@ -6,6 +6,9 @@
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/autograd/variable.h>
 
+#include <c10/hip/HIPStream.h>
+
+#include <cstdlib>
 #include <stdexcept>
 
 #include "../kernels/kernels.h"
@@ -28,6 +31,16 @@ struct ReducerState {
 
   std::vector<std::shared_ptr<torch::autograd::Node>> accumulators;
 
+  // comm timing (RCCL path only): first bucket start / last bucket end on the comm stream, and
+  // the end of backward compute on the caller's stream -> all-reduce time and its exposed tail
+  bool timing = false;
+  bool timed = false;  // events of the last finished iteration are valid
+  hipEvent_t ev_start = nullptr, ev_end = nullptr, ev_bwd = nullptr;
+  // debug: a gradient marked ready again after its bucket's all-reduce was issued means a kernel
+  // wrote into memory an in-flight collective reads -> error instead of a silent race
+  bool strict = false;
+  int64_t duplicate_marks = 0;
+
   std::mutex mu;
   bool enabled = true;
   bool expecting = false;
@@ -49,12 +62,14 @@ struct ReducerState {
   }
 
   void launch_bucket(int64_t b) {
+    const bool first = launch_order.empty();
     launch_order.push_back(b);
     if (comm) {
       const at::Tensor& f = flats[b];
       c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
       comm->comm_wait_current();
       hipStream_t cs = comm->stream();
+      if (timing && first) hipEventRecord(ev_start, cs);
       if (wire_bf16) {
         if (!wire[b].defined())
           wire[b] = at::empty({f.numel()}, f.options().dtype(at::kBFloat16));
@@ -82,7 +97,14 @@ struct ReducerState {
   }
 
   void mark_param(int64_t idx, bool zero_if_missing) {
-    if (param_ready[idx]) return;
+    if (param_ready[idx]) {
+      ++duplicate_marks;
+      if (strict && bucket_of[idx] < next_launch)
+        throw std::runtime_error("Reducer: gradient of parameter " + std::to_string(idx) +
+                                 " marked ready again after its bucket's all-reduce was issued "
+                                 "(write/collective race)");
+      return;
+    }
     param_ready[idx] = 1;
     at::Tensor& p = params[idx];
     const at::Tensor& v = views[idx];
@@ -126,6 +148,13 @@ struct ReducerState {
     for (size_t i = 0; i < params.size(); ++i)
       if (!param_ready[i]) mark_param((int64_t)i, /*zero_if_missing=*/true);
     if (comm) {
+      if (timing) {
+        c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
+        hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)comm->device()).stream();
+        hipEventRecord(ev_bwd, cur);
+        hipEventRecord(ev_end, comm->stream());
+        timed = !launch_order.empty();
+      }
       comm->current_wait_comm();
     } else {
       py::gil_scoped_acquire gil;
@@ -163,6 +192,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
     st_->members[b].push_back((int64_t)i);
   }
   st_->reset_counters();
+  if (const char* e = std::getenv("PDT_DEBUG_REDUCER")) st_->strict = e[0] == '1';
 
   std::weak_ptr<ReducerState> weak = st_;
   st_->self = weak;
@@ -180,7 +210,36 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   }
 }
 
-Reducer::~Reducer() = default;
+Reducer::~Reducer() {
+  for (hipEvent_t e : {st_->ev_start, st_->ev_end, st_->ev_bwd})
+    if (e) hipEventDestroy(e);
+}
+
+void Reducer::set_timing(bool on) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  if (on && !st_->comm) throw std::runtime_error("Reducer timing needs the RCCL communicator");
+  if (on && !st_->ev_start) {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->comm->device());
+    for (hipEvent_t* e : {&st_->ev_start, &st_->ev_end, &st_->ev_bwd})
+      if (hipEventCreate(e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
+  }
+  st_->timing = on;
+  st_->timed = false;
+}
+
+std::pair<double, double> Reducer::comm_timing() {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  if (!st_->timing || !st_->timed) return {-1.0, -1.0};
+  hipEventSynchronize(st_->ev_end);
+  hipEventSynchronize(st_->ev_bwd);
+  float total = 0.f, tail = 0.f;
+  hipEventElapsedTime(&total, st_->ev_start, st_->ev_end);
+  hipEventElapsedTime(&tail, st_->ev_bwd, st_->ev_end);
+  return {(double)total, tail > 0.f ? (double)tail : 0.0};
+}
+
+void Reducer::set_strict(bool on) { st_->strict = on; }
+int64_t Reducer::duplicate_marks() const { return st_->duplicate_marks; }
 
 void Reducer::prepare_for_backward() {
   std::lock_guard<std::mutex> lk(st_->mu);

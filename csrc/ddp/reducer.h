@@ -26,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../comm/rccl_comm.h"
@@ -50,6 +51,14 @@ class Reducer {
   int64_t num_buckets() const;
   std::vector<int64_t> last_launch_order() const;
   int64_t iterations() const;
+  // RCCL path: record events around each iteration's all-reduces; comm_timing() returns
+  // (ms from first bucket start to last bucket end, ms the all-reduce tail outlasted backward)
+  // of the last finished iteration, or (-1, -1).
+  void set_timing(bool on);
+  std::pair<double, double> comm_timing();
+  // error (instead of ignoring) when a gradient is marked ready after its bucket was launched
+  void set_strict(bool on);
+  int64_t duplicate_marks() const;
 
  private:
   std::shared_ptr<ReducerState> st_;

@@ -281,6 +281,36 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restr
   }
 }
 
+// stage 1 for partials produced by a BN-fused dgrad: block (32 channels, FIN_GPB groups),
+// fixed summation order -> ws[P][2][K] in the layout bn_bwd_reduce_stage2 consumes
+__global__ void __launch_bounds__(256) bn_bwd_part_stage1(const float* __restrict__ part, int G, int K,
+                                                          float* __restrict__ ws) {
+  __shared__ float sa[FIN_ROWS][FIN_CH + 1], sb[FIN_ROWS][FIN_CH + 1];
+  const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
+  const int k = blockIdx.x * FIN_CH + tx;
+  const int g0 = blockIdx.y * FIN_GPB;
+  const int g1 = min(G, g0 + FIN_GPB);
+  float a = 0.f, b = 0.f;
+  if (k < K) {
+#pragma unroll 4
+    for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
+      a += part[((int64_t)g * 2 + 0) * K + k];
+      b += part[((int64_t)g * 2 + 1) * K + k];
+    }
+  }
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && k < K) {
+    for (int r = 1; r < FIN_ROWS; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
+    float* o = ws + (int64_t)blockIdx.y * 2 * K;
+    o[k] = a;
+    o[K + k] = b;
+  }
+}
+
+size_t bn_bwd_part_ws_floats(int G, int K) { return (size_t)ceil_div(G, FIN_GPB) * 2 * K; }
+
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                               const float* stats, int mask, int64_t M, int K, float* ws,
                               float* sums, float* dgamma, float* dbeta, hipStream_t st) {
@@ -371,6 +401,14 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   else { PDT_BWD_T(0) }
 #undef PDT_BWD_T
 #undef PDT_BWD
+}
+
+void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float* sums,
+                               const float* invstd, float* dgamma, float* dbeta, hipStream_t st) {
+  const int P = ceil_div(G, FIN_GPB);
+  hipLaunchKernelGGL(bn_bwd_part_stage1, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws);
+  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, P, K, sums,
+                     invstd, dgamma, dbeta);
 }
 
 }  // namespace pdt

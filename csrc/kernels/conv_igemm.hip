@@ -33,6 +33,8 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -98,7 +100,20 @@ struct NtArgs {
   // A-coordinate offset (dr0 + i*dstep, ds0 + j*dstep).  Closed form -> pure scalar math in the
   // K loop (a per-tap table in kernel args would be read with vector loads every K-step).
   int ntaps, tnr, tns, tr0, ts0, tstep, dr0, ds0, dstep;
+  // EPI_BNB (dgrad): BN-backward of the unit that produced this conv's input, fused into the
+  // epilogue.  out = g = dx * relu'(unit) and per-(wave rows, channel) partials of
+  // (sum g, sum g*(y - mean)) go to bn_part[bn_group0 + wave_row_group][2][Nout].
+  const uint16_t* bn_y;   // that unit's pre-BN conv output (same layout as out)
+  const uint16_t* bn_z;   // its post-activation output (mask mode 1 only)
+  const float* bn_stats;  // [4][Nout] mean, invstd, scale, shift
+  float* bn_part;
+  int bn_mask, bn_group0;
 };
+
+// epilogue variants of the NT kernel
+constexpr int EPI_PLAIN = 0;  // store (+ optional addend)
+constexpr int EPI_STATS = 1;  // + BN forward partial statistics (conv fwd)
+constexpr int EPI_BNB = 2;    // + fused BN backward relu-mask and partial sums (conv dgrad)
 
 // LDS image of a [rows][64] bf16 tile: 128-B rows, 16-B chunk XOR-swizzled by (row>>1)&7.
 // For the 16x16x32 fragment read (lane l: row l&15, chunk 4*ksub + (l>>4)) every ds_read_b128
@@ -107,7 +122,7 @@ __device__ __forceinline__ int swz128(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int STAGES = 2>
 struct NtCfg {
   static constexpr int NT = WM * WN * 64;
   static constexpr int WAVES = WM * WN;
@@ -117,7 +132,8 @@ struct NtCfg {
   static constexpr int A_PW = BM / 8 / WAVES;  // instructions per wave per K-step
   static constexpr int B_PW = BN / 8 / WAVES;
   static_assert(A_PW * 8 * WAVES == BM && B_PW * 8 * WAVES == BN, "tile rows must split over waves");
-  static constexpr int PIPE_BYTES = 2 * (BM + BN) * 128;
+  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
   static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row (pixel)
   static constexpr int EPI_BYTES = WAVES * (TM * 16) * EPI_PITCH;
   static constexpr int SMEM = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
@@ -130,6 +146,28 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint
       r, (__attribute__((address_space(3))) void*)(reinterpret_cast<uintptr_t>(lds)), 16, voff, 0, 0, 0);
 }
 
+// Wait until at most N of this wave's vector-memory ops (LDS-DMA included) are outstanding.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Workgroup barrier WITHOUT the memory-model fence of __syncthreads(): that fence makes the compiler
+// emit s_waitcnt vmcnt(0) before s_barrier, draining every in-flight LDS-DMA and defeating a
+// multi-stage pipeline.  Callers order memory themselves: their own counted vmcnt wait covers the
+// DMA into the buffer about to be read, and every ds_read of the buffer about to be refilled has
+// been consumed (lgkmcnt 0) by the MFMAs before the barrier.  The "memory" clobber keeps the
+// compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// Multi-stage pipelines: every K-step issues LPS DMA ops per wave; wait until the oldest pending
+// step has landed while `younger` later steps (wave-uniform, < 3) may stay in flight.
+template <int LPS>
+__device__ __forceinline__ void wait_steps(int younger) {
+  if (younger >= 2) wait_vm<2 * LPS>();
+  else if (younger == 1) wait_vm<LPS>();
+  else wait_vm<0>();
+}
+
 // Main loop: LDS-DMA staging (no VGPR round trip, no ds_write), the XOR swizzle applied on the
 // SOURCE side (lane slot j of row r fetches chunk j ^ f(r)) so the lane-linear LDS image equals
 // the swizzled image swz128() reads.  Two buffers: the DMA of tile k+1 is issued before the MFMAs
@@ -137,9 +175,9 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint
 // MFMA operands are swapped (A = weights, B = pixels) so each lane's 4 accumulator registers are
 // 4 consecutive output channels of one pixel: the epilogue packs them into one 8-byte LDS write
 // and the BN statistics reduce over the 16 pixel-lanes with DPP-friendly xor shuffles.
-template <int WM, int WN, int TM, int TN, bool C64, bool STATS>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI>
 __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) {
-  using CFG = NtCfg<WM, WN, TM, TN>;
+  using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -243,13 +281,16 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  constexpr int LPS = A_PW + B_PW;
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nk) issue(p, p);
+  wait_steps<LPS>(min(nk, STAGES - 1) - 1);
+  lds_barrier();
+  int cur = 0, nxt = STAGES - 1;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
-    const char* As = smem + cur * (BM + BN) * 128;
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, nxt);
+    const char* As = smem + cur * CFG::STAGE_BYTES;
     const char* Bs = As + BM * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -266,8 +307,10 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    wait_steps<LPS>(min(nk - 1, kt + STAGES - 1) - (kt + 1));
+    lds_barrier();
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
   }
 
   // --------------------------------------------------------------- epilogue
@@ -275,7 +318,7 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
   const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
 
-  if constexpr (STATS) {
+  if constexpr (EPI == EPI_STATS) {
     // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels;
     // the writer converts to M2 about the group mean (cancellation is benign at 64 rows; groups
     // are combined with Chan's parallel formula in bn_finalize).
@@ -335,6 +378,20 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   __builtin_amdgcn_wave_barrier();
   constexpr int CH_PER_ROW = TN * 2;  // 16-B chunks per wave-tile row
   constexpr int CHUNKS = TM * 16 * CH_PER_ROW;
+  static_assert(64 % CH_PER_ROW == 0, "a lane keeps one channel chunk across the store loop");
+  // EPI_BNB: this lane's 8 channels are fixed (c = lane % CH_PER_ROW); per-lane partial sums
+  float bmu[8], bsc[8], bsh[8], bsg[8], bsq[8];
+  if constexpr (EPI == EPI_BNB) {
+    const int colb = min(wcol0 + (lane % CH_PER_ROW) * 8, P.Nout - 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      bmu[q] = P.bn_stats[colb + q];
+      bsc[q] = P.bn_stats[2 * P.Nout + colb + q];
+      bsh[q] = P.bn_stats[3 * P.Nout + colb + q];
+      bsg[q] = 0.f;
+      bsq[q] = 0.f;
+    }
+  }
   for (int qd = lane; qd < CHUNKS; qd += 64) {
     int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
     int m = wrow0 + r;
@@ -356,7 +413,44 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
         for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
         v = __builtin_bit_cast(v4i, pack8(a));
       }
+      if constexpr (EPI == EPI_BNB) {
+        // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
+        // partial sums agree bit for bit with what the apply pass reads back
+        f8 a = unpack8(__builtin_bit_cast(uint4, v));
+        const f8 yv = unpack8(*reinterpret_cast<const uint4*>(P.bn_y + orow * P.Nout + col));
+        f8 zv;
+        if (P.bn_mask == 1) zv = unpack8(*reinterpret_cast<const uint4*>(P.bn_z + orow * P.Nout + col));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const bool on = P.bn_mask == 1 ? zv.v[q] > 0.f
+                        : (P.bn_mask == 2 ? fmaf(yv.v[q], bsc[q], bsh[q]) > 0.f : true);
+          const float g = on ? a.v[q] : 0.f;
+          a.v[q] = g;
+          bsg[q] += g;
+          bsq[q] = fmaf(g, yv.v[q] - bmu[q], bsq[q]);
+        }
+        v = __builtin_bit_cast(v4i, pack8(a));
+      }
       *reinterpret_cast<v4i*>(P.out + orow * P.Nout + col) = v;
+    }
+  }
+  if constexpr (EPI == EPI_BNB) {
+    // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
+    // first CH_PER_ROW lanes write this wave's (rows group, channels) partials
+#pragma unroll
+    for (int o = CH_PER_ROW; o < 64; o <<= 1)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        bsg[q] += __shfl_xor(bsg[q], o, 64);
+        bsq[q] += __shfl_xor(bsq[q], o, 64);
+      }
+    const int colw = wcol0 + lane * 8;
+    if (lane < CH_PER_ROW && wrow0 < P.M && colw < P.Nout) {
+      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + wrow0 / (TM * 16)) * 2) * P.Nout + colw;
+      *reinterpret_cast<float4*>(pp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
+      *reinterpret_cast<float4*>(pp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
+      *reinterpret_cast<float4*>(pp + P.Nout) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
+      *reinterpret_cast<float4*>(pp + P.Nout + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
     }
   }
 }
@@ -413,15 +507,16 @@ __device__ __forceinline__ int swz_img(int row, int chunk) {
   else return swz128_tr(row, chunk);
 }
 
-template <int BMG, int BNG>
+template <int BMG, int BNG, int STAGES>
 struct TnCfg {
   static_assert(BNG == 128 && (BMG == 64 || BMG == 128), "TN tile shapes");
+  static_assert(STAGES >= 2 && STAGES <= 3, "pipeline depth");
   static constexpr int NT = 256;
   static constexpr int A_ROWB = BMG * 2;              // bytes per m row of the dy tile image
   static constexpr int A_BYTES = 64 * A_ROWB;
   static constexpr int B_BYTES = 64 * 256;            // [64 m][128 col], 256-B rows
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int SMEM = 2 * STAGE;              // 2 pipeline buffers
+  static constexpr int SMEM = STAGES * STAGE;
   static constexpr int TM = BMG / 2 / 16;             // 2x2 waves
   static constexpr int TN = BNG / 2 / 16;
   static constexpr int A_LPR = A_ROWB / 16;           // lanes per row in one 1-KiB DMA instruction
@@ -436,9 +531,9 @@ struct TnCfg {
 // Grid: 1-D over (split, tile) with split-major logical ids after the XCD remap, so the
 // column tiles of one split -- which read the same dy rows and overlapping x rows -- run on
 // the same XCD and share its L2.
-template <int BMG, int BNG, bool ATOMIC>
+template <int BMG, int BNG, int STAGES, bool ATOMIC>
 __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
-  using CFG = TnCfg<BMG, BNG>;
+  using CFG = TnCfg<BMG, BNG, STAGES>;
   constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -531,12 +626,18 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
     return base + swz256(row, col >> 3) + ((col & 7) << 1);
   };
 
-  if (s_begin < s_end) issue(s_begin, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int step = s_begin; step < s_end; ++step) {
-    const int cur = (step - s_begin) & 1;
-    if (step + 1 < s_end) issue(step + 1, cur ^ 1);
+  // STAGES-1 K-steps in flight ahead of the one being consumed; the buffer refilled at the top of
+  // iteration i is the one consumed in iteration i-1 (released by that iteration's barrier).
+  constexpr int LPS = A_PW + B_PW;
+  const int nst = s_end - s_begin;
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nst) issue(s_begin + p, p);
+  wait_steps<LPS>(min(nst, STAGES - 1) - 1);
+  lds_barrier();
+  int cur = 0, nxt = STAGES - 1;
+  for (int i = 0; i < nst; ++i) {
+    if (i + STAGES - 1 < nst) issue(s_begin + i + STAGES - 1, nxt);
     const char* As = smem + cur * CFG::STAGE;
     const char* Bs = As + CFG::A_BYTES;
 #pragma unroll
@@ -562,8 +663,10 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    wait_steps<LPS>(min(nst - 1, i + STAGES - 1) - (i + 1));
+    lds_barrier();
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
   }
 
   // epilogue: lane holds rows fq*4+e, column fr.  ATOMIC: fp32 atomic add into the zeroed dW
@@ -621,38 +724,78 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <int WM, int WN, int TM, int TN, bool C64, bool STATS>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI>
 static void run_nt(const NtArgs& a, hipStream_t st) {
-  using CFG = NtCfg<WM, WN, TM, TN>;
+  using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   int ntm = (a.M + CFG::BM - 1) / CFG::BM;
   int ntn = (a.Nout + CFG::BN - 1) / CFG::BN;
-  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, C64, STATS>;
+  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, STAGES, C64, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
     attr_set = true;
   }
-  // a single-step K loop never touches the second pipeline buffer: halve the LDS request so
-  // more blocks fit per CU (these short-K 1x1 convs are bound by their epilogue stores)
+  // a K loop shorter than the pipeline never touches the last buffers: request only the LDS it
+  // uses so more blocks fit per CU (the short-K 1x1 convs are bound by their epilogue stores)
   const int nk = C64 ? a.ntaps * (a.CA / 64) : (a.Kg + 63) / 64;
-  int smem = CFG::SMEM;
-  if (nk <= 1) smem = std::max(CFG::PIPE_BYTES / 2, CFG::EPI_BYTES);
+  const int smem = std::max(std::max(1, std::min(nk, STAGES)) * CFG::STAGE_BYTES, CFG::EPI_BYTES);
   hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), smem, st, a);
   check_launch("igemm_nt");
 }
 
-// tile choice: output channels 64 -> tall tile (more M rows per block); small M -> short tile
-template <bool C64, bool STATS>
+// Pipeline depth per NT tile (256x64, 64x128, 128x128); PDT_NT_STAGES="a,b,c" overrides.
+static int nt_stages(int which) {
+  static int v[3] = {-1, -1, -1};
+  if (v[0] < 0) {
+    v[0] = 2; v[1] = 2; v[2] = 2;
+    if (const char* e = getenv("PDT_NT_STAGES")) {
+      int x[3] = {2, 2, 2};
+      if (sscanf(e, "%d,%d,%d", &x[0], &x[1], &x[2]) == 3)
+        for (int k = 0; k < 3; ++k) v[k] = x[k] == 3 ? 3 : 2;
+    }
+  }
+  return v[which];
+}
+
+// Tile policy.  Per K-step a BMxBN tile issues (BM+BN)/8 1-KiB LDS-DMA instructions and reads
+// (TM+TN)/(TM*TN) KiB of LDS fragments per MFMA; the 256x256 tile (8 waves of 64x128) halves the
+// DMA issues and cuts fragment reads by a quarter per MFMA, but runs one block per CU, so it only
+// pays with enough blocks (>= 196, measured on the ResNet-50 shape classes: +10-20% on the 28x28
+// and 14x14 layers, -40% on 7x7 with 98 blocks) and a K loop longer than one step.
+// PDT_NT_TILE=1 disables it, =2 forces it wherever Nout >= 256 (tuning knob).
+static int nt_tile_mode() {
+  static int v = -1;
+  if (v < 0) {
+    v = 0;
+    if (const char* e = getenv("PDT_NT_TILE")) v = atoi(e);
+  }
+  return v;
+}
+
+static bool use_wide_tile(const NtArgs& a) {
+  const int mode = nt_tile_mode();
+  if (mode == 1 || a.Nout < 256) return false;
+  if (mode == 2) return true;
+  const int64_t blocks = (int64_t)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+  return a.Kg >= 128 && blocks >= 196;
+}
+
+// tile choice: output channels 64 -> tall tile (more M rows per block); small M -> short tile;
+// big GEMMs -> 256x256
+template <bool C64, int EPI>
 static void dispatch_nt(const NtArgs& a, hipStream_t st, int* group_rows) {
+  if (group_rows) *group_rows = (a.Nout > 64 && a.M <= 8192) ? 32 : 64;
   if (a.Nout <= 64) {
-    if (group_rows) *group_rows = 64;
-    run_nt<4, 1, 4, 4, C64, STATS>(a, st);       // 256 x 64
+    if (nt_stages(0) == 3) run_nt<4, 1, 4, 4, 3, C64, EPI>(a, st);  // 256 x 64
+    else run_nt<4, 1, 4, 4, 2, C64, EPI>(a, st);
   } else if (a.M <= 8192) {
-    if (group_rows) *group_rows = 32;
-    run_nt<2, 2, 2, 4, C64, STATS>(a, st);       // 64 x 128
+    if (nt_stages(1) == 3) run_nt<2, 2, 2, 4, 3, C64, EPI>(a, st);  // 64 x 128
+    else run_nt<2, 2, 2, 4, 2, C64, EPI>(a, st);
+  } else if (use_wide_tile(a)) {
+    run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);  // 256 x 256
   } else {
-    if (group_rows) *group_rows = 64;
-    run_nt<2, 2, 4, 4, C64, STATS>(a, st);       // 128 x 128
+    if (nt_stages(2) == 3) run_nt<2, 2, 4, 4, 3, C64, EPI>(a, st);  // 128 x 128
+    else run_nt<2, 2, 4, 4, 2, C64, EPI>(a, st);
   }
 }
 
@@ -683,18 +826,36 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   bool c64 = (s.C % 64) == 0;
   if (part) {
-    if (c64) dispatch_nt<true, true>(a, st, nullptr);
-    else dispatch_nt<false, true>(a, st, nullptr);
+    if (c64) dispatch_nt<true, EPI_STATS>(a, st, nullptr);
+    else dispatch_nt<false, EPI_STATS>(a, st, nullptr);
   } else {
-    if (c64) dispatch_nt<true, false>(a, st, nullptr);
-    else dispatch_nt<false, false>(a, st, nullptr);
+    if (c64) dispatch_nt<true, EPI_PLAIN>(a, st, nullptr);
+    else dispatch_nt<false, EPI_PLAIN>(a, st, nullptr);
   }
 }
 
+static int dgrad_class_rows(const ConvShape& s, int ph, int pw) {
+  const int str = s.stride;
+  const int Mi = (s.H - ph + str - 1) / str;
+  const int Mj = (s.W - pw + str - 1) / str;
+  return (Mi <= 0 || Mj <= 0) ? 0 : s.N * Mi * Mj;
+}
+
+int conv_dgrad_bn_groups(const ConvShape& s) {
+  int g = 0;
+  for (int ph = 0; ph < s.stride; ++ph)
+    for (int pw = 0; pw < s.stride; ++pw) {
+      const int M = dgrad_class_rows(s, ph, pw);
+      if (M > 0) g += ceil_div(M, conv_fwd_group_rows(M, s.C));
+    }
+  return g;
+}
+
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st) {
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn) {
   if (s.K % 64 != 0) throw std::runtime_error("conv_dgrad: output channels must be a multiple of 64");
   const int str = s.stride;
+  int group0 = 0;
   for (int ph = 0; ph < str; ++ph)
     for (int pw = 0; pw < str; ++pw) {
       NtArgs a{};
@@ -719,11 +880,31 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
       a.ntaps = a.tnr * a.tns;  // 0 -> kernel writes zeros for this class
       a.tr0 = r0; a.ts0 = s0; a.tstep = str;
       a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;
-      dispatch_nt<true, false>(a, st, nullptr);
+      if (bn != nullptr) {
+        a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part;
+        a.bn_mask = bn->mask; a.bn_group0 = group0;
+        group0 += ceil_div(a.M, conv_fwd_group_rows(a.M, a.Nout));
+        dispatch_nt<true, EPI_BNB>(a, st, nullptr);
+      } else {
+        dispatch_nt<true, EPI_PLAIN>(a, st, nullptr);
+      }
     }
 }
 
 // ------------------------------------------------------------------- wgrad
+// Pipeline depth per TN tile width; PDT_TN_STAGES="<bmg64>,<bmg128>" overrides (tuning knob).
+static int tn_stages(int bmg) {
+  static int st64 = -1, st128 = -1;
+  if (st64 < 0) {
+    st64 = 2; st128 = 2;
+    if (const char* e = getenv("PDT_TN_STAGES")) {
+      int a = 0, b = 0;
+      if (sscanf(e, "%d,%d", &a, &b) == 2) { st64 = a == 3 ? 3 : 2; st128 = b == 3 ? 3 : 2; }
+    }
+  }
+  return bmg == 64 ? st64 : st128;
+}
+
 struct WgradPlan {
   int bmg, bng, tiles, splits, steps_per_split, nsteps;
 };
@@ -756,10 +937,10 @@ size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
   return (size_t)p.splits * s.K * s.R * s.S * s.C;
 }
 
-template <int BMG, int BNG, bool ATOMIC>
+template <int BMG, int BNG, int STAGES, bool ATOMIC>
 static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
-  using CFG = TnCfg<BMG, BNG>;
-  auto kfn = igemm_tn_kernel<BMG, BNG, ATOMIC>;
+  using CFG = TnCfg<BMG, BNG, STAGES>;
+  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -790,12 +971,13 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.accumulate = accumulate ? 1 : 0;
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
+  const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
   if (p.bmg == 64) {
-    if (atomic) run_tn<64, 128, true>(a, p.tiles, p.splits, st);
-    else run_tn<64, 128, false>(a, p.tiles, p.splits, st);
+    if (deep) { if (atomic) run_tn<64, 128, 3, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 3, false>(a, p.tiles, p.splits, st); }
+    else { if (atomic) run_tn<64, 128, 2, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false>(a, p.tiles, p.splits, st); }
   } else {
-    if (atomic) run_tn<128, 128, true>(a, p.tiles, p.splits, st);
-    else run_tn<128, 128, false>(a, p.tiles, p.splits, st);
+    if (deep) { if (atomic) run_tn<128, 128, 3, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 3, false>(a, p.tiles, p.splits, st); }
+    else { if (atomic) run_tn<128, 128, 2, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 2, false>(a, p.tiles, p.splits, st); }
   }
   if (slab) {
     int64_t b = (n / 4 + 255) / 256;

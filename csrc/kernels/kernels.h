@@ -32,8 +32,21 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
                      const ConvShape& s, hipStream_t st);
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);
 // all stride/pad combos (stride > 1 as stride^2 parity classes)
+// Optional fused BatchNorm backward of the unit whose output x was (dx = dL/dx of that unit's
+// activation): the kernel stores g = dx * relu'(.) instead of dx (mask 0: none, 1: z > 0,
+// 2: y*scale + shift > 0) and writes per-row-group partials part[G][2][C] of
+// (sum g, sum g*(y - mean)), G = conv_dgrad_bn_groups(s); reduce them with
+// launch_bn_bwd_part_reduce.
+struct BnBwdFuse {
+  const uint16_t* y;     // [N,H,W,C] pre-BN output of that unit
+  const uint16_t* z;     // [N,H,W,C] its activation output (mask 1) or null
+  const float* stats;    // [4][C] mean, invstd, scale, shift
+  float* part;           // [G][2][C]
+  int mask;
+};
+int conv_dgrad_bn_groups(const ConvShape& s);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st);
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr);
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
@@ -62,6 +75,11 @@ void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift
 size_t bn_bwd_ws_floats(int64_t M, int K);
 // If dgamma/dbeta are non-null the final stage also accumulates dgamma += sum_gx*invstd and
 // dbeta += sum_g into them (parameter gradients written in place).
+// Reduce row-group partials part[G][2][K] (from a BN-fused dgrad) to sums[2][K]; ws holds
+// bn_bwd_part_ws_floats(G, K) floats.  Optional dgamma += sum_b*invstd, dbeta += sum_a.
+size_t bn_bwd_part_ws_floats(int G, int K);
+void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float* sums,
+                               const float* invstd, float* dgamma, float* dbeta, hipStream_t st);
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                               const float* stats, int mask, int64_t M, int K, float* ws,
                               float* sums, float* dgamma, float* dbeta, hipStream_t st);

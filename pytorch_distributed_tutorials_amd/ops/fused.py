@@ -266,19 +266,35 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     return z, y, stats
 
 
+class _BnHandoff:
+    """What a block leaves on its output tensor so the NEXT block's backward can run this
+    block's last BatchNorm backward (relu mask + reduction) inside its own input-gradient
+    dgrad epilogue.  The consumer deposits (g, sums); the producer uses them only if the
+    gradient it receives IS that g (same storage: no other consumer added to it)."""
+
+    __slots__ = ("y", "stats", "gamma", "beta", "deposit")
+
+    def __init__(self, y, stats, gamma, beta):
+        self.y, self.stats, self.gamma, self.beta = y, stats, gamma, beta
+        self.deposit = None
+
+
 class _ResidualBlock(torch.autograd.Function):
     """z = relu(unit_n(...unit_1(x)) + shortcut(x)) with unit = conv -> BN -> (ReLU).
 
     One autograd node per block lets backward fuse across units: the shortcut
     gradient is summed into the block-input gradient inside the first conv's
-    dgrad epilogue (no separate add kernel), and units are processed in one
-    straight-line sequence of native launches.
+    dgrad epilogue (no separate add kernel); each unit's BatchNorm backward
+    (ReLU mask and the per-channel reduction) runs inside the epilogue of the dgrad
+    that produces its input gradient (``conv_dgrad_bn``), including -- through a
+    ``_BnHandoff`` -- the previous block's last unit; the remaining per-unit pass is
+    one elementwise apply.
     tensors = per unit (w, gamma, beta, running_mean, running_var), chain units
     first, then the downsample unit if present.
     """
 
     @staticmethod
-    def forward(ctx, x, spec, *tensors):
+    def forward(ctx, x, spec, handoff, *tensors):
         C = native()
         chain, ds_cfg = spec
         nch = len(chain)
@@ -307,6 +323,10 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.params = tensors  # the Parameter objects: gradients may be written into flat views
         ctx.spec = spec
         ctx.ntensors = len(tensors)
+        ctx.handoff_in = handoff  # the producer of x (previous block), or None
+        _, y_last, st_last = outs[-1]
+        ctx.handoff_out = _BnHandoff(y_last, st_last, tensors[5 * (nch - 1) + 1],
+                                     tensors[5 * (nch - 1) + 2])
         return h
 
     @staticmethod
@@ -348,20 +368,58 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j + 1] = sums_[1] * stt_[1]
                 grads[j + 2] = sums_[0]
             return sums_
+
+        def dgrad_bn(j, dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_):
+            """input gradient of a conv + BN backward reduction of unit j (its producer)"""
+            sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
+            if sg is not None and sb is not None:
+                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_,
+                                            sg, sb)
+                sunk.extend([params[j + 1], params[j + 2]])
+            else:
+                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_)
+                grads[j + 1] = sums_[1] * stt_[1]
+                grads[j + 2] = sums_[0]
+            return g_, sums_
+
+        # gradient arriving pre-masked and pre-reduced from the next block's dgrad epilogue?
+        pre = None
+        ho = ctx.handoff_out
+        if ho.deposit is not None:
+            g_dep, sums_dep = ho.deposit
+            ho.deposit = None
+            jl = 5 * (nch - 1)
+            if g_dep.data_ptr() == dz.data_ptr() and g_dep.shape == dz.shape:
+                pre = (dz, sums_dep)
+                sunk.extend([params[jl + 1], params[jl + 2]])
+            else:  # another consumer contributed: undo the deposited BN-parameter gradients
+                inv = units[nch - 1][2][1]
+                with torch.no_grad():
+                    _grad_sink(params[jl + 1]).sub_(sums_dep[1] * inv)
+                    _grad_sink(params[jl + 2]).sub_(sums_dep[0])
+        ctx.handoff_out = None
+
         for i in reversed(range(nch)):
             st, pd, tr, mo, ep = chain[i]
             z, y, stt = units[i]
             w, gamma = tensors[5 * i], tensors[5 * i + 1]
             xin = x if i == 0 else units[i - 1][0]
             last = i == nch - 1
-            mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
-            sums = bnreduce(5 * i, dz, z, y, stt, mask)
-            dy, dres = C.bn_act_bwd_apply(dz, z, y, stt, gamma, sums, mask, tr, last)
+            if pre is None:
+                mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
+                sums = bnreduce(5 * i, dz, z, y, stt, mask)
+                dy, dres = C.bn_act_bwd_apply(dz, z, y, stt, gamma, sums, mask, tr, last)
+            else:
+                g, sums = pre  # g = dz * relu'(unit i), reduced in the producing epilogue
+                dy, _ = C.bn_act_bwd_apply(g, g, y, stt, gamma, sums, 0, tr, False)
+                dres = g
+            pre = None
             wgrad(5 * i, dy, xin, st, pd)
             if last:
                 g_short = dres
             if i > 0:
-                dz = C.conv_dgrad(dy, w, list(xin.shape), st, pd)
+                yp, sttp = units[i - 1][1], units[i - 1][2]
+                pre = dgrad_bn(5 * (i - 1), dy, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
             else:
                 # shortcut gradient: identity -> g_short itself; projection -> its dgrad
                 if ds_cfg is not None:
@@ -374,10 +432,23 @@ class _ResidualBlock(torch.autograd.Function):
                     addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2)
                 else:
                     addend = g_short
-                dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend) if ctx.needs_input_grad[0] else None
+                if not ctx.needs_input_grad[0]:
+                    dz = None
+                else:
+                    hi = ctx.handoff_in
+                    sg = _grad_sink(hi.gamma) if hi is not None else None
+                    sb = _grad_sink(hi.beta) if hi is not None else None
+                    if sg is not None and sb is not None and x.shape[3] % 8 == 0:
+                        # previous block's last unit: relu mask from its output z = x
+                        dz, sums_in = C.conv_dgrad_bn(dy, w, list(x.shape), st, pd, addend, hi.y, x,
+                                                      hi.stats, 1, sg, sb)
+                        hi.deposit = (dz, sums_in)
+                    else:
+                        dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend)
+        ctx.handoff_in = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
-        return (dz, None, *grads)
+        return (dz, None, None, *grads)
 
 
 def _grad_sink(p):
@@ -402,4 +473,9 @@ def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
         tr, mo, ep = _bn_prepare(bn)
         ds_spec = (conv.stride[0], conv.padding[0], tr, mo, ep)
         tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
-    return _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec), *tensors)
+    out = _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec), getattr(x, "_pdt_handoff", None),
+                               *tensors)
+    node = out.grad_fn  # the ctx of this block's node (None without autograd)
+    if node is not None and getattr(node, "handoff_out", None) is not None:
+        out._pdt_handoff = node.handoff_out
+    return out

@@ -283,6 +283,29 @@ class DistributedDataParallel(nn.Module):
         finally:
             self.require_backward_grad_sync = old
 
+    # ------------------------------------------------------------- metrics
+    def enable_comm_timing(self, on: bool = True) -> bool:
+        """Record HIP events around each iteration's all-reduces (native RCCL path only)."""
+        if self.reducer is None or self.comm is None or not hasattr(self.reducer, "set_timing"):
+            return False
+        self.reducer.set_timing(on)
+        self._timing = on
+        return True
+
+    def comm_stats(self) -> Optional[dict]:
+        """All-reduce time of the last iteration and the part of it backward did not hide."""
+        if not getattr(self, "_timing", False):
+            return None
+        total, exposed = self.reducer.comm_timing()
+        if total < 0:
+            return None
+        return {"comm_ms": total, "exposed_ms": exposed}
+
+    def abort(self) -> None:
+        """Abort the native communicator (unblocks kernels waiting on a dead peer)."""
+        if self.comm is not None:
+            self.comm.abort()
+
     def bucket_info(self) -> dict:
         return {"num_buckets": len(self.bucket_ranges), "bucket_elems": list(self.bucket_sizes),
                 "native_comm": self.comm is not None,

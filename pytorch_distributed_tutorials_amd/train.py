@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import argparse
 import os
-import time
 from typing import Optional
 
 import torch
@@ -32,7 +31,10 @@ from .models import build_model
 from .optim import SGD
 from .parallel import DistributedDataParallel, destroy, init_distributed
 from .utils.checkpoint import load_checkpoint, save_checkpoint
+from .utils import trace
+from .utils.metrics import StepTimer
 from .utils.seed import set_random_seeds
+from .utils.watchdog import FaultInjector, Watchdog
 
 DEFAULTS = {
     "num_epochs": 10000,
@@ -77,6 +79,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-steps-per-epoch", type=int, default=None)
     p.add_argument("--timeout", type=float, default=None, help="collective timeout (s)")
     p.add_argument("--log-every", type=int, default=0, help="print img/s every N steps (0 = off)")
+    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
+                   help="compute dtype: native kernels are bf16 (fp32 master weights); the torch "
+                        "path runs fp32 (reference) or bf16 autocast; auto = bf16 native / fp32 torch")
+    p.add_argument("--steps", type=int, default=None, help="stop after this many training steps in total")
+    p.add_argument("--trace", action="store_true",
+                   help="emit roctx ranges (fwd/bwd/step/eval) for rocprofv3 --marker-trace")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="abort this rank when a step makes no progress for N seconds (0 = off)")
     p.add_argument("--deterministic", action=argparse.BooleanOptionalAction, default=True,
                    help="bitwise-reproducible kernels (reference sets cudnn.deterministic=True); "
                         "--no-deterministic enables atomic split-K weight gradients")
@@ -107,6 +117,14 @@ def main(argv: Optional[list] = None) -> int:
     impl = args.impl
     if impl == "auto":
         impl = "native" if device.type == "cuda" else "torch"
+    dtype = args.dtype
+    if dtype == "auto":
+        dtype = "bf16" if impl == "native" else "fp32"
+    if impl == "native" and dtype != "bf16":
+        raise SystemExit("--impl native computes in bf16 (fp32 master weights); use --impl torch for fp32")
+    autocast = (impl == "torch" and dtype == "bf16")
+    if args.trace:
+        trace.enable(True)
 
     model = build_model(args.arch, num_classes=args.num_classes, impl=impl).to(device)
     if impl == "native":
@@ -115,6 +133,13 @@ def main(argv: Optional[list] = None) -> int:
                                         output_device=local_rank if use_cuda else None,
                                         bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
     criterion = ops.CrossEntropyLoss() if impl == "native" else nn.CrossEntropyLoss()
+    timer = StepTimer(device, ddp_model)
+    if args.log_every:
+        ddp_model.enable_comm_timing(True)
+    watchdog = None
+    if args.watchdog_timeout > 0:
+        watchdog = Watchdog(args.watchdog_timeout, rank=env.rank, on_timeout=ddp_model.abort)
+    inject = FaultInjector(env.rank)
     optimizer = SGD(ddp_model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
 
     model_filepath = os.path.join(args.model_dir, args.model_filename)
@@ -137,10 +162,15 @@ def main(argv: Optional[list] = None) -> int:
                                 device=device, seed=args.seed + env.rank)
     test_loader = DeviceLoader(test_set, 128, shuffle=False, augment=False, device=device)
 
+    global_step = 0
+    done = False
     for epoch in range(start_epoch, args.num_epochs):
         print("Local Rank: {}, Epoch: {}, Training ...".format(local_rank, epoch), flush=True)
         if epoch % args.eval_every == 0 and local_rank == 0:
-            accuracy = evaluate(model=ddp_model, device=device, test_loader=test_loader)
+            if watchdog is not None:
+                watchdog.heartbeat("eval")
+            with trace.trace_range("eval"):
+                accuracy = evaluate(model=ddp_model, device=device, test_loader=test_loader)
             save_checkpoint(ddp_model, model_filepath, optimizer, epoch)
             print("-" * 75)
             print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
@@ -148,22 +178,39 @@ def main(argv: Optional[list] = None) -> int:
 
         ddp_model.train()
         train_loader.set_epoch(epoch)
-        t0 = time.perf_counter()
+        timer.start()
         for step, (inputs, labels) in enumerate(train_loader):
             if args.max_steps_per_epoch is not None and step >= args.max_steps_per_epoch:
                 break
+            if args.steps is not None and global_step >= args.steps:
+                done = True
+                break
+            if watchdog is not None:
+                watchdog.heartbeat(f"epoch {epoch} step {step}")
+            inject(global_step)
             inputs, labels = inputs.to(device), labels.to(device)
             optimizer.zero_grad()
-            outputs = ddp_model(inputs)
-            loss = criterion(outputs, labels)
-            loss.backward()
-            optimizer.step()
-            if args.log_every and (step + 1) % args.log_every == 0 and env.rank == 0:
-                if device.type == "cuda":
-                    torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-                print(f"  step {step + 1} loss {loss.item():.4f} "
-                      f"{(step + 1) * args.batch_size * env.world_size / dt:.1f} img/s", flush=True)
+            with trace.trace_range("forward"), torch.autocast(device.type, torch.bfloat16, enabled=autocast):
+                outputs = ddp_model(inputs)
+                loss = criterion(outputs, labels)
+            with trace.trace_range("backward"):
+                loss.backward()
+            with trace.trace_range("optimizer"):
+                optimizer.step()
+            timer.tick()
+            global_step += 1
+            if args.log_every and (step + 1) % args.log_every == 0:
+                r = timer.report()
+                if env.rank == 0 and r is not None:
+                    msg = (f"  step {step + 1} loss {loss.item():.4f} {r['step_ms']:.2f} ms/step "
+                           f"{args.batch_size * env.world_size * 1000.0 / r['step_ms']:.1f} img/s")
+                    if "comm_ms" in r:
+                        msg += f" allreduce {r['comm_ms']:.2f} ms (exposed {r['exposed_ms']:.2f} ms)"
+                    print(msg, flush=True)
+        if done:
+            break
+    if watchdog is not None:
+        watchdog.stop()
     destroy()
     return 0
 
