@@ -520,5 +520,6 @@ PYBIND11_MODULE(_C, m) {
       .def("set_timing", &pdt::Reducer::set_timing)
       .def("comm_timing", &pdt::Reducer::comm_timing, py::call_guard<py::gil_scoped_release>())
       .def("set_strict", &pdt::Reducer::set_strict)
+      .def("set_aux_stream", &pdt::Reducer::set_aux_stream)
       .def_property_readonly("duplicate_marks", &pdt::Reducer::duplicate_marks);
 }

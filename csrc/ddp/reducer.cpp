@@ -40,6 +40,10 @@ struct ReducerState {
   // wrote into memory an in-flight collective reads -> error instead of a silent race
   bool strict = false;
   int64_t duplicate_marks = 0;
+  // side stream that produces some gradients (weight-gradient GEMMs run there, concurrent with
+  // the input-gradient chain): every bucket all-reduce also waits for it
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_aux = nullptr;
 
   std::mutex mu;
   bool enabled = true;
@@ -69,6 +73,10 @@ struct ReducerState {
       c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
       comm->comm_wait_current();
       hipStream_t cs = comm->stream();
+      if (aux) {
+        hipEventRecord(ev_aux, aux);
+        hipStreamWaitEvent(cs, ev_aux, 0);
+      }
       if (timing && first) hipEventRecord(ev_start, cs);
       if (wire_bf16) {
         if (!wire[b].defined())
@@ -211,7 +219,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
 }
 
 Reducer::~Reducer() {
-  for (hipEvent_t e : {st_->ev_start, st_->ev_end, st_->ev_bwd})
+  for (hipEvent_t e : {st_->ev_start, st_->ev_end, st_->ev_bwd, st_->ev_aux})
     if (e) hipEventDestroy(e);
 }
 
@@ -239,6 +247,17 @@ std::pair<double, double> Reducer::comm_timing() {
 }
 
 void Reducer::set_strict(bool on) { st_->strict = on; }
+
+void Reducer::set_aux_stream(uintptr_t stream) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  if (!st_->comm) throw std::runtime_error("Reducer aux stream needs the RCCL communicator");
+  if (!st_->ev_aux) {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->comm->device());
+    if (hipEventCreateWithFlags(&st_->ev_aux, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("hipEventCreate failed");
+  }
+  st_->aux = reinterpret_cast<hipStream_t>(stream);
+}
 int64_t Reducer::duplicate_marks() const { return st_->duplicate_marks; }
 
 void Reducer::prepare_for_backward() {

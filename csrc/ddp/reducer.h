@@ -26,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <cstdint>
 #include <utility>
 #include <vector>
 
@@ -58,6 +59,8 @@ class Reducer {
   std::pair<double, double> comm_timing();
   // error (instead of ignoring) when a gradient is marked ready after its bucket was launched
   void set_strict(bool on);
+  // bucket all-reduces additionally wait for this stream (gradients produced on a side stream)
+  void set_aux_stream(uintptr_t stream);
   int64_t duplicate_marks() const;
 
  private:

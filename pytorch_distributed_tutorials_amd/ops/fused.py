@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import reference as ref
+from . import streams
 from ..utils.seed import deterministic
 from ._ext import native
 
@@ -349,11 +350,19 @@ class _ResidualBlock(torch.autograd.Function):
         params = ctx.params
         sunk = []  # parameters whose gradient was accumulated in place into the flat buffer
 
+        side = streams.begin(x.device)
+
         def wgrad(j, dy_, xin_, st_, pd_):
             w_ = tensors[j]
             sink = _grad_sink(params[j])
             if sink is not None:
-                C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det, sink)
+                # weight gradient into the flat buffer on the side stream, concurrent with the
+                # dgrad chain; all-reduce and optimizer wait for that stream (streams.py)
+                if side is not None:
+                    streams.launch(side, lambda: C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_,
+                                                              det, sink), dy_, xin_)
+                else:
+                    C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det, sink)
                 sunk.append(params[j])
             else:
                 grads[j] = C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det).to(w_.dtype)

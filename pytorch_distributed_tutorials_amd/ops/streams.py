@@ -1,0 +1,62 @@
+"""Side stream for weight-gradient GEMMs.
+
+In a conv unit's backward the input-gradient (dgrad) and weight-gradient (wgrad)
+GEMMs are independent.  Issuing wgrad on a second HIP stream lets the two fill
+each other's partial waves: a 7x7 or 14x14 layer launches fewer workgroups than
+the chip has CUs, and every GEMM ends in a tail where CUs drain.  The dgrad chain
+stays on the caller's stream (it is the critical path of backward).
+
+Ordering: the side stream waits for the caller's stream before each wgrad (its
+inputs are ready); the inputs are ``record_stream``-ed so the caching allocator
+does not hand their memory out while the side stream still reads them; gradient
+all-reduces wait for the side stream (``Reducer.set_aux_stream``); and a callback
+at the end of backward joins it into the caller's stream, so the optimizer step
+sees every gradient.  ``PDT_WGRAD_STREAM=0`` turns it off.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+
+_enabled = os.environ.get("PDT_WGRAD_STREAM", "1") != "0"
+_streams: Dict[int, torch.cuda.Stream] = {}
+
+
+def set_enabled(on: bool) -> None:
+    global _enabled
+    _enabled = on
+
+
+def wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
+    if not _enabled or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _streams[idx] = s
+    return s
+
+
+def begin(device: torch.device) -> Optional[torch.cuda.Stream]:
+    """Called inside a backward that will put work on the side stream: queues the join of the
+    side stream into the caller's stream at the end of this backward pass."""
+    s = wgrad_stream(device)
+    if s is None:
+        return None
+    cur = torch.cuda.current_stream(device)
+    torch.autograd.Variable._execution_engine.queue_callback(lambda: cur.wait_stream(s))
+    return s
+
+
+def launch(side: torch.cuda.Stream, fn, *inputs: torch.Tensor):
+    """Run ``fn()`` on the side stream after the caller's stream reached this point; keeps the
+    (caller-stream-allocated) ``inputs`` alive for the side stream's reads."""
+    side.wait_stream(torch.cuda.current_stream(side.device))
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in inputs:
+        t.record_stream(side)
+    return out

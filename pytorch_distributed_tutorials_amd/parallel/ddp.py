@@ -210,6 +210,11 @@ class DistributedDataParallel(nn.Module):
                                           self._py_launch, self._py_finalize)
             self._flats = flats
             self.space.reducer = self.reducer
+            if self.comm is not None:
+                from ..ops import streams
+                side = streams.wgrad_stream(self.device)
+                if side is not None:  # weight gradients are produced on a side stream
+                    self.reducer.set_aux_stream(side.cuda_stream)
 
     # ------------------------------------------------------------- helpers
     def _verify_params_across_processes(self, params) -> None:
