@@ -143,15 +143,26 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& wk, int64_t s
   return {y, part};
 }
 
+// wt: optional pre-packed bf16 [C][R][S][K] weights (flat-space dgrad mirror)
+Tensor packed_t_or_pack(const Tensor& w, const std::optional<Tensor>& wt) {
+  if (wt.has_value() && wt->defined()) {
+    TORCH_CHECK(wt->scalar_type() == at::kBFloat16 && wt->is_contiguous() && wt->dim() == 4 &&
+                wt->size(0) == w.size(1) && wt->size(1) == w.size(2) && wt->size(2) == w.size(3) &&
+                wt->size(3) == w.size(0), "wt must be bf16 [C,R,S,K] contiguous");
+    return *wt;
+  }
+  return pack_weight_t(w);
+}
+
 Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, int64_t stride,
-                  int64_t pad, const std::optional<Tensor>& addend) {
+                  int64_t pad, const std::optional<Tensor>& addend, const std::optional<Tensor>& wt_in) {
   check_bf16_nhwc(dy, "dy");
   TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
   TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
   c10::hip::HIPGuard g(dy.get_device());
   auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
-  Tensor wt = pack_weight_t(w);
+  Tensor wt = packed_t_or_pack(w, wt_in);
   auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
   const uint16_t* ap = nullptr;
   if (addend.has_value() && addend->defined()) {
@@ -172,7 +183,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
                                          const std::optional<Tensor>& addend, const Tensor& y,
                                          const std::optional<Tensor>& z, const Tensor& stats,
                                          int64_t mask, const std::optional<Tensor>& dgamma,
-                                         const std::optional<Tensor>& dbeta) {
+                                         const std::optional<Tensor>& dbeta,
+                                         const std::optional<Tensor>& wt_in) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(y, "y");
   TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
@@ -192,7 +204,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
     TORCH_CHECK(z->sizes() == y.sizes(), "z shape mismatch");
     zp = cbf(*z);
   }
-  Tensor wt = pack_weight_t(w);
+  Tensor wt = packed_t_or_pack(w, wt_in);
   auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
   const uint16_t* ap = nullptr;
   if (addend.has_value() && addend->defined()) {
@@ -424,7 +436,8 @@ Tensor top1_correct(const Tensor& logits_in, const Tensor& labels) {
 
 // --------------------------------------------------------------------- sgd
 void sgd_step(Tensor p, const Tensor& g, Tensor buf, double lr, double momentum, double dampening,
-              double wd, bool nesterov, bool first, double grad_scale) {
+              double wd, bool nesterov, bool first, double grad_scale,
+              const std::optional<Tensor>& p_bf16) {
   check_cuda(p, "param");
   check_cuda(g, "grad");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 flat buffers only");
@@ -437,11 +450,44 @@ void sgd_step(Tensor p, const Tensor& g, Tensor buf, double lr, double momentum,
   auto aligned = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   TORCH_CHECK(aligned(p.data_ptr()) && aligned(g.data_ptr()) && (!mom || aligned(buf.data_ptr())),
               "sgd_step: flat buffers must be 16-byte aligned");
+  uint16_t* pb = nullptr;
+  if (p_bf16.has_value() && p_bf16->defined()) {
+    check_cuda(*p_bf16, "p_bf16");
+    TORCH_CHECK(p_bf16->scalar_type() == at::kBFloat16 && p_bf16->numel() == p.numel(),
+                "sgd_step: bf16 mirror must match the parameter buffer");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(p_bf16->data_ptr()) & 15) == 0, "mirror must be 16-B aligned");
+    pb = bf(*p_bf16);
+  }
   c10::hip::HIPGuard gd(p.get_device());
   pdt::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), mom ? buf.data_ptr<float>() : nullptr,
                   p.numel(), (float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first,
-                  (float)grad_scale, cur_stream(p));
+                  (float)grad_scale, cur_stream(p), pb);
 }
+
+// flat fp32 -> bf16 mirror (refresh when parameters changed outside the fused SGD step)
+void cast_to_bf16(const Tensor& x, Tensor y) {
+  check_cuda(x, "x");
+  check_cuda(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kBFloat16 && x.numel() == y.numel(),
+              "cast_to_bf16: fp32 -> bf16 of equal size");
+  c10::hip::HIPGuard gd(x.get_device());
+  pdt::launch_cast_f32_bf16(x.data_ptr<float>(), bf(y), x.numel(), cur_stream(x));
+}
+
+// table: int64 [n][4] = (offset, K, C, RS) on the device; src/dst: flat bf16 mirrors
+void pack_t_batched(const Tensor& src, Tensor dst, const Tensor& table, int64_t max_tiles) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kByte && table.is_contiguous(),
+              "pack_t_batched: table must be a device byte tensor");
+  const int64_t eb = (int64_t)pdt::pack_t_entry_bytes();
+  TORCH_CHECK(table.numel() % eb == 0, "pack_t_batched: table size");
+  c10::hip::HIPGuard gd(src.get_device());
+  pdt::launch_pack_t_batched(cbf(src), bf(dst), table.data_ptr(), (int)(table.numel() / eb),
+                             (int)max_tiles, cur_stream(src));
+}
+
+int64_t pack_t_entry_bytes() { return (int64_t)pdt::pack_t_entry_bytes(); }
 
 }  // namespace
 
@@ -453,11 +499,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", checked("conv_fwd", &conv_fwd), py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("stats"));
   m.def("conv_dgrad", checked("conv_dgrad", &conv_dgrad), py::arg("dy"), py::arg("w"), py::arg("x_shape"), py::arg("stride"),
-        py::arg("pad"), py::arg("addend") = py::none());
+        py::arg("pad"), py::arg("addend") = py::none(), py::arg("wt") = py::none());
   m.def("conv_dgrad_bn", checked("conv_dgrad_bn", &conv_dgrad_bn), py::arg("dy"), py::arg("w"),
         py::arg("x_shape"), py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("y"),
         py::arg("z"), py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(),
-        py::arg("dbeta") = py::none());
+        py::arg("dbeta") = py::none(), py::arg("wt") = py::none());
   m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
   m.def("bn_finalize", checked("bn_finalize", &bn_finalize));
@@ -473,7 +519,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool_bwd", checked("avgpool_bwd", &avgpool_bwd));
   m.def("softmax_xent", checked("softmax_xent", &softmax_xent));
   m.def("top1_correct", checked("top1_correct", &top1_correct));
-  m.def("sgd_step", checked("sgd_step", &sgd_step));
+  m.def("sgd_step", checked("sgd_step", &sgd_step), py::arg("p"), py::arg("g"), py::arg("buf"),
+        py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
+        py::arg("first"), py::arg("grad_scale"), py::arg("p_bf16") = py::none());
+  m.def("cast_to_bf16", checked("cast_to_bf16", &cast_to_bf16));
+  m.def("pack_t_batched", checked("pack_t_batched", &pack_t_batched));
+  m.def("pack_t_entry_bytes", &pack_t_entry_bytes);
   m.def("conv_fwd_group_rows", &pdt::conv_fwd_group_rows);
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });

@@ -15,6 +15,12 @@ void launch_image_to_nhwc(const float* x, uint16_t* y, int N, int C, int H, int 
 void launch_pack_weight(const float* w, const int64_t* strides, uint16_t* out, int K, int C,
                         int R, int S, int Cp, hipStream_t st);
 // fp32 weight [K][C][R][S] -> bf16 [C][R][S][K] (dgrad B operand; no flip, taps indexed explicitly)
+// batched CRSK pack of many KRSC bf16 weights living in one flat mirror (same offsets in dst);
+// table = device array of ntensors entries of pack_t_entry_bytes() bytes:
+// {int64 off; int K, C, RS, tiles_k = ceil(K/64), tiles_c = ceil(C/64)}; K, C multiples of 8
+void launch_pack_t_batched(const uint16_t* src, uint16_t* dst, const void* table, int ntensors,
+                           int max_tiles, hipStream_t st);
+size_t pack_t_entry_bytes();
 void launch_pack_weight_t(const float* w, const int64_t* strides, uint16_t* out, int K, int C,
                           int R, int S, hipStream_t st);
 
@@ -109,7 +115,7 @@ void launch_top1(const float* logits, const int64_t* labels, int64_t* count, int
 // torch.optim.SGD on flat fp32 buffers; grad is scaled by grad_scale first.
 void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
                 float dampening, float wd, bool nesterov, bool first, float grad_scale,
-                hipStream_t st);
+                hipStream_t st, uint16_t* p_bf16 = nullptr);
 // fp32 -> bf16 cast (used for bf16 gradient buckets) and back
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t st);

@@ -84,4 +84,64 @@ void launch_pack_weight_t(const float* w, const int64_t* strides, uint16_t* out,
                      w, ws, out, K, C, R, S);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batched dgrad-layout pack: for every conv weight of a flat parameter space, the bf16 KRSC mirror
+// slice src[off .. off + K*RS*C) (written by the fused SGD step) is transposed to CRSK at
+// dst[off ..].  One launch for all layers: blockIdx.y = tensor, blockIdx.x walks that tensor's
+// (tap, 64-k, 64-c) tiles; a 64x64 tile goes through LDS so reads (c-contiguous) and writes
+// (k-contiguous) are both 16-B vectors.
+struct PackTEntry { int64_t off; int K, C, RS, tiles_k, tiles_c; };
+
+__global__ void __launch_bounds__(256) pack_t_batched_kernel(const uint16_t* __restrict__ src,
+                                                             uint16_t* __restrict__ dst,
+                                                             const PackTEntry* __restrict__ tab) {
+  __shared__ uint16_t tile[64][64 + 8];
+  const PackTEntry e = tab[blockIdx.y];
+  const int per_tap = e.tiles_k * e.tiles_c;
+  const int ntiles = e.RS * per_tap;
+  const int t = threadIdx.x;
+  for (int tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+    const int tap = tile_id / per_tap;
+    const int rem = tile_id - tap * per_tap;
+    const int tk = rem / e.tiles_c, tc = rem - (rem / e.tiles_c) * e.tiles_c;
+    const int k0 = tk * 64, c0 = tc * 64;
+    // read 64 k-rows x 64 c (8 lanes per row, 8 bf16 each)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = it * 32 + (t >> 3), cc = (t & 7) * 8;
+      const int k = k0 + row, c = c0 + cc;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (k < e.K && c < e.C)
+        v = *reinterpret_cast<const uint4*>(src + e.off + ((int64_t)k * e.RS + tap) * e.C + c);
+      const uint16_t* pv = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tile[row][cc + q] = pv[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = it * 32 + (t >> 3), kk = (t & 7) * 8;  // row = c within tile
+      const int c = c0 + row, k = k0 + kk;
+      if (c < e.C && k < e.K) {
+        uint16_t o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = tile[kk + q][row];
+        *reinterpret_cast<uint4*>(dst + e.off + ((int64_t)c * e.RS + tap) * e.K + k) =
+            *reinterpret_cast<const uint4*>(o);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void launch_pack_t_batched(const uint16_t* src, uint16_t* dst, const void* table, int ntensors,
+                           int max_tiles, hipStream_t st) {
+  if (ntensors <= 0) return;
+  const int bx = max_tiles < 512 ? max_tiles : 512;
+  hipLaunchKernelGGL(pack_t_batched_kernel, dim3(bx > 0 ? bx : 1, ntensors), dim3(256), 0, st, src,
+                     dst, reinterpret_cast<const PackTEntry*>(table));
+}
+
+size_t pack_t_entry_bytes() { return sizeof(PackTEntry); }
+
 }  // namespace pdt

@@ -12,11 +12,13 @@
 
 namespace pdt {
 
-template <bool MOM, bool NEST>
+// MIRROR: also write bf16(p') to pb -- the KRSC bf16 weights the next forward's convs consume
+// (conv weights are channels_last, so the flat fp32 order already is KRSC), saving a pack pass.
+template <bool MOM, bool NEST, bool MIRROR>
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ buf, int64_t n, float lr,
                                                   float mom, float damp1, float wd, bool first,
-                                                  float scale) {
+                                                  float scale, uint16_t* __restrict__ pb) {
   int64_t n4 = n / 4;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -35,29 +37,39 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const f
     step(pv.x, gv.x, bv.x); step(pv.y, gv.y, bv.y); step(pv.z, gv.z, bv.z); step(pv.w, gv.w, bv.w);
     reinterpret_cast<float4*>(p)[i] = pv;
     if (MOM) reinterpret_cast<float4*>(buf)[i] = bv;
+    if (MIRROR) reinterpret_cast<uint2*>(pb)[i] = make_uint2(pack2bf(pv.x, pv.y), pack2bf(pv.z, pv.w));
   }
   for (int64_t i = n4 * 4 + tid; i < n; i += stride) {
     float pv = p[i], bv = MOM ? buf[i] : 0.f;
     step(pv, g[i], bv);
     p[i] = pv;
     if (MOM) buf[i] = bv;
+    if (MIRROR) pb[i] = f2bf(pv);
   }
 }
 
-void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
-                float dampening, float wd, bool nesterov, bool first, float grad_scale,
-                hipStream_t st) {
+template <bool MIRROR>
+static void launch_sgd_t(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
+                         float dampening, float wd, bool nesterov, bool first, float grad_scale,
+                         hipStream_t st, uint16_t* pb) {
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
   dim3 gr((unsigned)blocks), bl(256);
   float damp1 = 1.f - dampening;
   if (momentum == 0.f)
-    hipLaunchKernelGGL((sgd_kernel<false, false>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale);
+    hipLaunchKernelGGL((sgd_kernel<false, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
   else if (nesterov)
-    hipLaunchKernelGGL((sgd_kernel<true, true>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale);
+    hipLaunchKernelGGL((sgd_kernel<true, true, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
   else
-    hipLaunchKernelGGL((sgd_kernel<true, false>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale);
+    hipLaunchKernelGGL((sgd_kernel<true, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
+}
+
+void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
+                float dampening, float wd, bool nesterov, bool first, float grad_scale,
+                hipStream_t st, uint16_t* p_bf16) {
+  if (p_bf16) launch_sgd_t<true>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, grad_scale, st, p_bf16);
+  else launch_sgd_t<false>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, grad_scale, st, nullptr);
 }
 
 __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restrict__ x,

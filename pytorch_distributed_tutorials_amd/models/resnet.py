@@ -180,6 +180,11 @@ class ResNet(nn.Module):
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
         # NCHW fp32 image (or an NHWC bf16 tensor already prepared by the data
         # pipeline) -> NHWC bf16 with C padded to the kernels' 8-channel granule.
+        if x.is_cuda:  # bf16 conv-weight mirror of the DDP flat space (refreshed if stale)
+            sp = getattr(self.conv1.weight, "_pdt_flat", None)
+            mirror = sp.mirror() if sp is not None else None
+            if mirror is not None:
+                mirror.ensure()
         if x.dim() == 4 and x.shape[1] == 3:
             x = ops.image_to_nhwc(x)
         x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)

@@ -253,11 +253,31 @@ def _bn_prepare(bn: nn.BatchNorm2d):
     return training, (momentum if momentum is not None else 0.0), bn.eps
 
 
+def _mirror_of(w):
+    sp = getattr(w, "_pdt_flat", None)
+    return sp._mirror if sp is not None else None
+
+
+def _packed_krsc(C, w, cx):
+    """bf16 [K,R,S,Cx] forward weights: a view of the flat-space mirror when current, else a pack."""
+    m = _mirror_of(w)
+    v = m.krsc_view(w) if m is not None else None
+    if v is not None and v.shape[3] == cx:
+        return v
+    return C.pack_weight(w, cx)
+
+
+def _packed_crsk(w):
+    """bf16 [C,R,S,K] dgrad weights from the mirror, or None (the binding packs)."""
+    m = _mirror_of(w)
+    return m.crsk_view(w) if m is not None else None
+
+
 def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual):
     k, _, r, s = w.shape
     n, h, wd, cx = x.shape
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
-    wk = C.pack_weight(w, cx)
+    wk = _packed_krsc(C, w, cx)
     y, part = C.conv_fwd(x, wk, stride, pad, training)
     if training:
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
@@ -383,10 +403,11 @@ class _ResidualBlock(torch.autograd.Function):
             sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
             if sg is not None and sb is not None:
                 g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_,
-                                            sg, sb)
+                                            sg, sb, _packed_crsk(w_))
                 sunk.extend([params[j + 1], params[j + 2]])
             else:
-                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_)
+                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_,
+                                            wt=_packed_crsk(w_))
                 grads[j + 1] = sums_[1] * stt_[1]
                 grads[j + 2] = sums_[0]
             return g_, sums_
@@ -438,7 +459,7 @@ class _ResidualBlock(torch.autograd.Function):
                     dy_ds, _ = C.bn_act_bwd_apply(g_short, g_short, y_ds, st_ds, gds, sums_ds,
                                                   0, tr2, False)
                     wgrad(5 * nch, dy_ds, x, st2, pd2)
-                    addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2)
+                    addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2, wt=_packed_crsk(wds))
                 else:
                     addend = g_short
                 if not ctx.needs_input_grad[0]:
@@ -450,10 +471,10 @@ class _ResidualBlock(torch.autograd.Function):
                     if sg is not None and sb is not None and x.shape[3] % 8 == 0:
                         # previous block's last unit: relu mask from its output z = x
                         dz, sums_in = C.conv_dgrad_bn(dy, w, list(x.shape), st, pd, addend, hi.y, x,
-                                                      hi.stats, 1, sg, sb)
+                                                      hi.stats, 1, sg, sb, _packed_crsk(w))
                         hi.deposit = (dz, sums_in)
                     else:
-                        dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend)
+                        dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend, _packed_crsk(w))
         ctx.handoff_in = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)

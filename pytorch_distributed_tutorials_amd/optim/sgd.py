@@ -81,8 +81,11 @@ class SGD(torch.optim.Optimizer):
                         self.state[p]["momentum_buffer"] = torch.as_strided(buf, p.shape, p.stride(), o)
                     first = not self._restored_momentum(sp)
                 buf = self._flat_bufs.get(key)
+                mirror = sp.mirror()
                 native().sgd_step(sp.param_flat, sp.grad_flat, buf, lr, mom, damp, wd, nest,
-                                  first, 1.0)
+                                  first, 1.0, mirror.krsc if mirror is not None else None)
+                if mirror is not None:
+                    mirror.after_optimizer_step()  # bf16 conv weights for the next forward
                 continue
             params, grads, bufs, firsts = [], [], [], []
             for p in group["params"]:

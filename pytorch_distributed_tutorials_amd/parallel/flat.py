@@ -12,7 +12,7 @@ bucket order.  Consequences:
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -47,6 +47,8 @@ class FlatParamSpace:
         self.grad_views: List[torch.Tensor] = []
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.reducer = None  # set by DistributedDataParallel when gradients are all-reduced
+        self.version = 0     # bumped by the fused optimizer step (raw writes bump no torch counter)
+        self._mirror = None
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 view = torch.as_strided(self.param_flat, p.shape, p.stride(), o)
@@ -94,6 +96,12 @@ class FlatParamSpace:
         if self.reducer is not None:
             self.reducer.mark_ready_external([self.index[id(p)] for p in params])
 
+    def mirror(self) -> "Optional[WeightMirror]":
+        """bf16 conv-weight mirror (GPU spaces only), created on first use."""
+        if self._mirror is None and self.param_flat.is_cuda:
+            self._mirror = WeightMirror(self)
+        return self._mirror
+
     def zero_grad(self) -> None:
         self.grad_flat.zero_()
         self.attach_grads()
@@ -101,6 +109,88 @@ class FlatParamSpace:
     def slice(self, start: int, end: int, which: str = "grad") -> torch.Tensor:
         buf = self.grad_flat if which == "grad" else self.param_flat
         return buf.narrow(0, start, end - start)
+
+
+class WeightMirror:
+    """bf16 copies of a flat space's conv weights in the two layouts the conv kernels read.
+
+    * ``krsc``: same offsets as the fp32 flat buffer; conv weights are channels_last, so the
+      flat fp32 order already IS [K][R][S][C] and the fused SGD step writes this mirror as a
+      side output (``sgd_step(..., p_bf16=)``): the forward convs need no pack launches;
+    * ``crsk``: the dgrad layout [C][R][S][K], produced for ALL layers by ONE batched transpose
+      launch after each optimizer step (instead of one pack kernel per layer per backward).
+    Validity key = (space.version, param_flat._version, sum of the conv weights' versions): our
+    optimizer bumps the first; a torch in-place write to a parameter (load_state_dict, user code)
+    bumps that parameter's own counter.
+    """
+
+    def __init__(self, space: "FlatParamSpace"):
+        import numpy as np
+        from ..ops._ext import native
+        self.space = space
+        C = native()
+        dev = space.param_flat.device
+        self.krsc = torch.empty(space.numel, dtype=torch.bfloat16, device=dev)
+        self.crsk = torch.empty(space.numel, dtype=torch.bfloat16, device=dev)
+        self._krsc_views: Dict[int, torch.Tensor] = {}
+        self._crsk_views: Dict[int, torch.Tensor] = {}
+        self._tracked: List[torch.nn.Parameter] = []
+        ent = []
+        for p, o in zip(space.params, space.offsets):
+            if p.dim() != 4:
+                continue
+            k, c, r, s_ = p.shape
+            want = (r * s_ * c, 1, s_ * c, c)  # KRSC-dense; a size-1 dim may carry any stride
+            krsc = all(n == 1 or st == wst for n, st, wst in zip(p.shape, p.stride(), want))
+            if k % 8 or c % 8 or not krsc:
+                continue  # e.g. the C=3 stem: packed per call with channel padding
+            self._tracked.append(p)
+            self._krsc_views[id(p)] = self.krsc.narrow(0, o, p.numel()).view(k, r, s_, c)
+            self._crsk_views[id(p)] = self.crsk.narrow(0, o, p.numel()).view(c, r, s_, k)
+            ent.append((o, k, c, r * s_, (k + 63) // 64, (c + 63) // 64, 0))
+        dt = np.dtype([("off", "<i8"), ("K", "<i4"), ("C", "<i4"), ("RS", "<i4"), ("tk", "<i4"),
+                       ("tc", "<i4"), ("pad", "<i4")])
+        assert dt.itemsize == C.pack_t_entry_bytes(), "PackTEntry layout mismatch"
+        arr = np.array(ent, dtype=dt)
+        self.table = torch.from_numpy(arr.view(np.uint8).copy()).to(dev)
+        self.ntensors = len(ent)
+        self.max_tiles = max((e[3] * e[4] * e[5] for e in ent), default=0)
+        self.key = None
+
+    def current_key(self):
+        # a Parameter re-homed with ``p.data = view`` keeps its own version counter
+        return (self.space.version, self.space.param_flat._version,
+                sum(p._version for p in self._tracked))
+
+    def _pack_t(self) -> None:
+        from ..ops._ext import native
+        if self.ntensors:
+            native().pack_t_batched(self.krsc, self.crsk, self.table, self.max_tiles)
+
+    def refresh(self) -> None:
+        from ..ops._ext import native
+        native().cast_to_bf16(self.space.param_flat, self.krsc)
+        self._pack_t()
+        self.key = self.current_key()
+
+    def ensure(self) -> None:
+        if self.key != self.current_key():
+            self.refresh()
+
+    def after_optimizer_step(self) -> None:
+        """The fused SGD step just wrote ``krsc``; rebuild ``crsk`` and mark both current."""
+        self.space.version += 1
+        self._pack_t()
+        self.key = self.current_key()
+
+    def valid(self) -> bool:
+        return self.key is not None and self.key == self.current_key()
+
+    def krsc_view(self, p) -> Optional[torch.Tensor]:
+        return self._krsc_views.get(id(p)) if self.valid() else None
+
+    def crsk_view(self, p) -> Optional[torch.Tensor]:
+        return self._crsk_views.get(id(p)) if self.valid() else None
 
 
 def flatten_buffers(module: torch.nn.Module) -> Dict[torch.dtype, torch.Tensor]:
