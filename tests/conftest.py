@@ -29,3 +29,11 @@ def gpu(native_ext):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 that is free right now (for launcher rendezvous in tests)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

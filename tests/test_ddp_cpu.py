@@ -13,13 +13,14 @@ import subprocess
 import sys
 
 import pytest
+from conftest import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _run(tmp_path, extra, nproc=2, timeout=420):
     out = str(tmp_path / "res")
-    port = random.randint(20000, 40000)
+    port = free_port()
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env["OMP_NUM_THREADS"] = "2"

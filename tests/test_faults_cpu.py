@@ -11,6 +11,7 @@ import sys
 import time
 
 import pytest
+from conftest import free_port
 import torch
 
 from pytorch_distributed_tutorials_amd.utils import trace
@@ -30,7 +31,7 @@ def _env(**extra):
 
 
 def _launch(tmp_path, extra_args, **env):
-    port = random.randint(20000, 40000)
+    port = free_port()
     cmd = [sys.executable, "-m", "pytorch_distributed_tutorials_amd.launch", "--nproc_per_node=2",
            "--master_port", str(port),
            "--arch", "resnet18", "--data", "synthetic-cifar", "--synthetic-samples", "64",

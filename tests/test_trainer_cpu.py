@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 import pytest
+from conftest import free_port
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,7 +38,7 @@ def test_trainer_single_process(tmp_path):
 
 @pytest.mark.slow
 def test_trainer_two_ranks_via_launcher(tmp_path):
-    port = random.randint(20000, 40000)
+    port = free_port()
     cmd = [sys.executable, "-m", "pytorch_distributed_tutorials_amd.launch", "--nproc_per_node=2",
            "--master_port", str(port), "--use-local-rank-arg",
            "--arch", "resnet18", "--data", "synthetic-cifar", "--synthetic-samples", "64",
