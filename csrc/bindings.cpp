@@ -270,6 +270,80 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
   return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
 }
 
+// -------------------------------------------------------------------- stem
+// 7x7/s2 stem with C <= 4 input channels as a super-pixel conv (kernels.h): returns
+// (xsp, y, part) -- xsp is the bf16 super-pixel image (kept for the weight gradient)
+std::tuple<Tensor, Tensor, Tensor> stem_conv_fwd(const Tensor& x, const Tensor& w, int64_t stride,
+                                                 int64_t pad, bool stats) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "stem: image must be fp32 NCHW");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4, "stem: weight must be fp32 4-D");
+  TORCH_CHECK(stride == 2 && x.size(1) <= 4 && w.size(1) == x.size(1), "stem: stride 2, <= 4 channels");
+  c10::hip::HIPGuard g(x.get_device());
+  Tensor xc = x.contiguous();
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int K = w.size(0), R = w.size(2), S = w.size(3);
+  const int Ho = (H + 2 * pad - R) / 2 + 1, Wo = (W + 2 * pad - S) / 2 + 1;
+  const int Sp = (S + 2) / 2, Hp = H + 2 * pad, Wsp = Wo + Sp - 1;
+  TORCH_CHECK(2 * (Ho - 1) + R <= Hp, "stem: padded height too small");
+  auto xsp = at::empty({N, Hp, Wsp, 8}, x.options().dtype(at::kBFloat16));
+  hipStream_t st = cur_stream(x);
+  pdt::launch_stem_image(xc.data_ptr<float>(), bf(xsp), N, C, H, W, (int)pad, Hp, Wsp, st);
+  auto wsp = at::empty({K, R, Sp, 8}, w.options().dtype(at::kBFloat16));
+  int64_t ws[4] = {w.stride(0), w.stride(1), w.stride(2), w.stride(3)};
+  pdt::launch_stem_pack_weight(w.data_ptr<float>(), ws, bf(wsp), K, C, R, S, Sp, st);
+  pdt::ConvShape s;
+  s.N = N; s.H = Hp; s.W = Wsp; s.C = 8; s.K = K; s.R = R; s.S = Sp;
+  s.Ho = Ho; s.Wo = Wo; s.stride = 2; s.stride_w = 1; s.pad = 0;
+  TORCH_CHECK(xsp.numel() < (int64_t(1) << 30), "stem: image too large for 32-bit addressing");
+  auto y = at::empty({N, Ho, Wo, K}, xsp.options());
+  Tensor part;
+  float* pp = nullptr;
+  if (stats) {
+    const int M = N * Ho * Wo;
+    const int grows = pdt::conv_fwd_group_rows(M, K);
+    part = at::empty({(M + grows - 1) / grows, 2, K}, x.options());
+    pp = part.data_ptr<float>();
+  }
+  pdt::launch_conv_fwd(cbf(xsp), cbf(wsp), bf(y), pp, s, st);
+  return {xsp, y, part};
+}
+
+// weight gradient of the stem from the super-pixel image; accumulates into `out` (fp32 [K,C,R,S],
+// any strides) when given, else returns a fresh channels_last tensor
+Tensor stem_wgrad(const Tensor& dy, const Tensor& xsp, std::vector<int64_t> wsz, bool deterministic,
+                  const std::optional<Tensor>& out) {
+  check_bf16_nhwc(dy, "dy");
+  check_bf16_nhwc(xsp, "xsp");
+  TORCH_CHECK(wsz.size() == 4, "weight shape must be [K,C,R,S]");
+  c10::hip::HIPGuard g(dy.get_device());
+  const int K = wsz[0], C = wsz[1], R = wsz[2], S = wsz[3];
+  const int Sp = (S + 2) / 2;
+  pdt::ConvShape s;
+  s.N = xsp.size(0); s.H = xsp.size(1); s.W = xsp.size(2); s.C = 8; s.K = K; s.R = R; s.S = Sp;
+  s.Ho = dy.size(1); s.Wo = dy.size(2); s.stride = 2; s.stride_w = 1; s.pad = 0;
+  TORCH_CHECK(dy.size(3) == K && s.Wo + Sp - 1 == s.W, "stem_wgrad: shape mismatch");
+  auto fopt = dy.options().dtype(at::kFloat);
+  size_t wsn = pdt::conv_wgrad_ws_floats(s, deterministic);
+  Tensor wsb = wsn ? at::empty({(int64_t)wsn}, fopt) : Tensor();
+  auto dwsp = at::empty({K, R, Sp, 8}, fopt);
+  hipStream_t st = cur_stream(dy);
+  pdt::launch_conv_wgrad(cbf(dy), cbf(xsp), dwsp.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
+                         s, deterministic, false, st);
+  Tensor o;
+  bool acc = false;
+  if (out.has_value() && out->defined()) {
+    o = *out;
+    TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
+                o.size(2) == R && o.size(3) == S, "stem_wgrad out: bad shape/dtype");
+    acc = true;
+  } else {
+    o = at::empty({K, C, R, S}, fopt.memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  int64_t os[4] = {o.stride(0), o.stride(1), o.stride(2), o.stride(3)};
+  pdt::launch_stem_wgrad_unpack(dwsp.data_ptr<float>(), o.data_ptr<float>(), os, K, C, R, S, Sp, acc, st);
+  return o;
+}
+
 // ---------------------------------------------------------------------- BN
 Tensor bn_finalize(const Tensor& part, int64_t count, const Tensor& rm, const Tensor& rv,
                    const Tensor& gamma, const Tensor& beta, double momentum, double eps) {
@@ -506,6 +580,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta") = py::none(), py::arg("wt") = py::none());
   m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
+  m.def("stem_conv_fwd", checked("stem_conv_fwd", &stem_conv_fwd), py::arg("x"), py::arg("w"),
+        py::arg("stride"), py::arg("pad"), py::arg("stats"));
+  m.def("stem_wgrad", checked("stem_wgrad", &stem_wgrad), py::arg("dy"), py::arg("xsp"),
+        py::arg("w_shape"), py::arg("deterministic") = false, py::arg("out") = py::none());
   m.def("bn_finalize", checked("bn_finalize", &bn_finalize));
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),

@@ -464,7 +464,7 @@ struct TnArgs {
   float* out;          // [splits][Kout][Ncols] (or dw directly when splits == 1)
   uint32_t dy_bytes, x_bytes;
   int Mred, Kout, Ncols;
-  int H, W, C, S, stride, pad;
+  int H, W, C, S, stride, pad, stride_w;
   FastDiv div_hw, div_w;  // m -> n = m / (Ho*Wo), ho = rem / Wo
   int HoWo, Wo;
   int steps_per_split, nsteps;
@@ -600,7 +600,7 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
       const uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
       const uint32_t ho = fdiv(rem, P.div_w);
       const uint32_t wo = rem - ho * (uint32_t)P.Wo;
-      const int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride + b_dw[i];
+      const int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride_w + b_dw[i];
       const bool ok = b_ok[i] && m < P.Mred && (unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W;
       const int off = (int)n * HWC2 + h * WC2 + w * C2 + b_chb[i];
       glds16(rx, Bs + (wid * B_PW + i) * 1024, ok ? (uint32_t)off : OOB);
@@ -818,7 +818,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.Nout = s.K; a.Kg = s.R * s.S * s.C; a.S = s.S;
   a.M = s.N * s.Ho * s.Wo;
   fill_common(a, s.Ho, s.Wo);
-  a.ash = s.stride; a.asw = s.stride; a.aoff_h = -s.pad; a.aoff_w = -s.pad;
+  a.ash = s.stride; a.asw = s.sw(); a.aoff_h = -s.pad; a.aoff_w = -s.pad;
   a.OH = s.Ho; a.OW = s.Wo; a.osh = 1; a.osw = 1; a.oph = 0; a.opw = 0;
   a.dense = 1;
   a.tnr = s.R; a.tns = s.S; a.ntaps = s.R * s.S;
@@ -962,7 +962,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.dy_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
   a.x_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
   a.Mred = s.N * s.Ho * s.Wo; a.Kout = s.K; a.Ncols = s.R * s.S * s.C;
-  a.H = s.H; a.W = s.W; a.C = s.C; a.S = s.S; a.stride = s.stride; a.pad = s.pad;
+  a.H = s.H; a.W = s.W; a.C = s.C; a.S = s.S; a.stride = s.stride; a.pad = s.pad; a.stride_w = s.sw();
   a.HoWo = s.Ho * s.Wo; a.Wo = s.Wo;
   a.div_hw = make_fastdiv((uint32_t)a.HoWo);
   a.div_w = make_fastdiv((uint32_t)s.Wo);

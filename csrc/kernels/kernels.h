@@ -21,6 +21,19 @@ void launch_pack_weight(const float* w, const int64_t* strides, uint16_t* out, i
 void launch_pack_t_batched(const uint16_t* src, uint16_t* dst, const void* table, int ntensors,
                            int max_tiles, hipStream_t st);
 size_t pack_t_entry_bytes();
+// Stem (7x7/s2, C <= 4) as a "super-pixel" conv: pairs of horizontally adjacent input pixels
+// become one 8-channel pixel (4 channels each), the 7 horizontal taps fold into 4 tap pairs, and
+// the image is pre-padded, so the conv is R x 4 taps, stride (2, 1), pad 0, C = 8:
+// K_gemm = 7*4*8 = 224 instead of 7*7*8 = 392, and no bounds checks in the A loads.
+// xsp[N][H+2pad][Wsp][q*4+c] = x[n][c][hp-pad][2*ws+q-pad-1] (0 outside / c >= C)
+void launch_stem_image(const float* x, uint16_t* xsp, int N, int C, int H, int W, int pad, int Hp,
+                       int Wsp, hipStream_t st);
+// wsp[k][r][p][q*4+c] = w[k][c][r][2p+q-1] (0 outside), w fp32 with strides
+void launch_stem_pack_weight(const float* w, const int64_t* strides, uint16_t* wsp, int K, int C,
+                             int R, int S, int Sp, hipStream_t st);
+// out[k][c][r][s] (+)= dwsp[k][r][(s+1)/2][((s+1)%2)*4+c], out channels_last (strides k:CRS... given)
+void launch_stem_wgrad_unpack(const float* dwsp, float* out, const int64_t* strides, int K, int C,
+                              int R, int S, int Sp, bool accumulate, hipStream_t st);
 void launch_pack_weight_t(const float* w, const int64_t* strides, uint16_t* out, int K, int C,
                           int R, int S, hipStream_t st);
 
@@ -30,6 +43,8 @@ struct ConvShape {
   int K, R, S;         // filter: K outputs, RxS taps
   int Ho, Wo;          // output spatial
   int stride, pad;
+  int stride_w = 0;    // horizontal stride when different from `stride` (fwd and wgrad only)
+  int sw() const { return stride_w > 0 ? stride_w : stride; }
 };
 // y[N,Ho,Wo,K] = conv(x, w[K][R][S][C]); if part != nullptr also writes per-group
 // BN partials part[ceil(M/G)][2][K] = (sum, M2 about the group mean), G = conv_fwd_group_rows().

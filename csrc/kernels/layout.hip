@@ -144,4 +144,88 @@ void launch_pack_t_batched(const uint16_t* src, uint16_t* dst, const void* table
 
 size_t pack_t_entry_bytes() { return sizeof(PackTEntry); }
 
+// ------------------------------------------------------------------------------------ stem
+// one thread per output super-pixel (8 bf16 = 16 B store); reads the <= 8 source floats
+__global__ void __launch_bounds__(256) stem_image_kernel(const float* __restrict__ x,
+                                                         uint16_t* __restrict__ xsp, int N, int C,
+                                                         int H, int W, int pad, int Hp, int Wsp) {
+  const int64_t total = (int64_t)N * Hp * Wsp;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ws = (int)(i % Wsp);
+  const int64_t t = i / Wsp;
+  const int hp = (int)(t % Hp);
+  const int n = (int)(t / Hp);
+  const int h = hp - pad;
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int w = 2 * ws + q - pad - 1;
+    const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      v[q * 4 + c] = (in && c < C) ? x[(((int64_t)n * C + c) * H + h) * W + w] : 0.f;
+  }
+  uint4 o;
+  o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+  o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+  reinterpret_cast<uint4*>(xsp)[i] = o;
+}
+
+void launch_stem_image(const float* x, uint16_t* xsp, int N, int C, int H, int W, int pad, int Hp,
+                       int Wsp, hipStream_t st) {
+  const int64_t total = (int64_t)N * Hp * Wsp;
+  hipLaunchKernelGGL(stem_image_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, xsp,
+                     N, C, H, W, pad, Hp, Wsp);
+}
+
+__global__ void stem_pack_weight_kernel(const float* __restrict__ w, WStrides ws,
+                                        uint16_t* __restrict__ out, int K, int C, int R, int S,
+                                        int Sp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = K * R * Sp * 8;
+  if (i >= total) return;
+  const int cq = i % 8, q = cq / 4, c = cq % 4;
+  int t = i / 8;
+  const int p = t % Sp; t /= Sp;
+  const int r = t % R;
+  const int k = t / R;
+  const int s = 2 * p + q - 1;
+  const float v = (c < C && s >= 0 && s < S) ? w[k * ws.k + c * ws.c + r * ws.r + s * ws.s] : 0.f;
+  out[i] = f2bf(v);
+}
+
+void launch_stem_pack_weight(const float* w, const int64_t* strides, uint16_t* wsp, int K, int C,
+                             int R, int S, int Sp, hipStream_t st) {
+  WStrides ws{strides[0], strides[1], strides[2], strides[3]};
+  const int total = K * R * Sp * 8;
+  hipLaunchKernelGGL(stem_pack_weight_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, ws, wsp,
+                     K, C, R, S, Sp);
+}
+
+__global__ void stem_wgrad_unpack_kernel(const float* __restrict__ dwsp, float* __restrict__ out,
+                                         WStrides os, int K, int C, int R, int S, int Sp,
+                                         int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = K * C * R * S;
+  if (i >= total) return;
+  const int s = i % S;
+  int t = i / S;
+  const int r = t % R; t /= R;
+  const int c = t % C;
+  const int k = t / C;
+  const int p = (s + 1) >> 1, q = (s + 1) & 1;
+  const float v = dwsp[((k * R + r) * Sp + p) * 8 + q * 4 + c];
+  float* o = out + k * os.k + c * os.c + r * os.r + s * os.s;
+  *o = accumulate ? *o + v : v;
+}
+
+void launch_stem_wgrad_unpack(const float* dwsp, float* out, const int64_t* strides, int K, int C,
+                              int R, int S, int Sp, bool accumulate, hipStream_t st) {
+  WStrides os{strides[0], strides[1], strides[2], strides[3]};
+  const int total = K * C * R * S;
+  hipLaunchKernelGGL(stem_wgrad_unpack_kernel, dim3((total + 255) / 256), dim3(256), 0, st, dwsp, out,
+                     os, K, C, R, S, Sp, accumulate ? 1 : 0);
+}
+
 }  // namespace pdt

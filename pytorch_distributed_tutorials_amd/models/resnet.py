@@ -185,9 +185,12 @@ class ResNet(nn.Module):
             mirror = sp.mirror() if sp is not None else None
             if mirror is not None:
                 mirror.ensure()
-        if x.dim() == 4 and x.shape[1] == 3:
-            x = ops.image_to_nhwc(x)
-        x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
+        if x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.is_floating_point():
+            x = ops.stem_conv_bn(x, self.conv1, self.bn1)  # super-pixel stem (fused.py)
+        else:
+            if x.dim() == 4 and x.shape[1] == 3:
+                x = ops.image_to_nhwc(x)
+            x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
         x = ops.maxpool3x3s2(x)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

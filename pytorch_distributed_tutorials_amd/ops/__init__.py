@@ -15,5 +15,6 @@ from .fused import (  # noqa: F401
     maxpool3x3s2,
     residual_block,
     set_cpu_activation_dtype,
+    stem_conv_bn,
     top1_correct,
 )

@@ -122,6 +122,69 @@ class _ConvBN(torch.autograd.Function):
                 None, None, None, None, None, None, None, None)
 
 
+class _StemConvBN(torch.autograd.Function):
+    """Device stem: NCHW fp32 image -> conv 7x7/s2 -> BN -> ReLU as a super-pixel conv.
+
+    The image is re-laid out so pairs of horizontally adjacent pixels form one 8-channel
+    "super-pixel" (3 channels + pad each), the seven horizontal taps fold into four tap pairs,
+    and the image is pre-padded: the implicit GEMM has K = 7*4*8 = 224 (vs 7*7*8 = 392 with
+    channel padding alone) and no bounds checks.  The image itself needs no gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, pad, training,
+                momentum, eps):
+        C = native()
+        xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
+        k = weight.shape[0]
+        count = y.shape[0] * y.shape[1] * y.shape[2]
+        if training:
+            if running_mean is None:
+                running_mean = torch.zeros(k, device=x.device)
+                running_var = torch.ones(k, device=x.device)
+            stats = C.bn_finalize(part, count, running_mean, running_var, gamma, beta,
+                                  float(momentum), float(eps))
+        else:
+            stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
+        z = C.bn_act_fwd(y, stats[2], stats[3], None, True)
+        ctx.save_for_backward(xsp, y, stats, gamma)
+        ctx.weight = weight
+        ctx.training = training
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        C = native()
+        xsp, y, stats, gamma = ctx.saved_tensors
+        weight = ctx.weight
+        dz = dz.contiguous()
+        sums = C.bn_act_bwd_reduce(dz, dz, y, stats, 2)
+        dgamma, dbeta = sums[1] * stats[1], sums[0]
+        dy, _ = C.bn_act_bwd_apply(dz, dz, y, stats, gamma, sums, 2, ctx.training, False)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            sink = _grad_sink(weight)
+            if sink is not None:
+                C.stem_wgrad(dy, xsp, list(weight.shape), deterministic(), sink)
+                weight._pdt_flat.mark_ready([weight])
+            else:
+                dw = C.stem_wgrad(dy, xsp, list(weight.shape), deterministic()).to(weight.dtype)
+        ctx.weight = None
+        return (None, dw, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, None, None, None,
+                None, None, None)
+
+
+def stem_conv_bn(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d) -> torch.Tensor:
+    """z = relu(BN(conv7x7/s2(image))) -> NHWC bf16, device path for <= 4-channel fp32 images.
+    Falls back to image_to_nhwc + conv_bn when the image itself needs a gradient."""
+    if (not x.is_cuda or x.requires_grad or x.dim() != 4 or x.shape[1] > 4 or conv.stride != (2, 2)
+            or conv.kernel_size[0] != conv.kernel_size[1] or conv.bias is not None):
+        return conv_bn(image_to_nhwc(x), conv, bn, relu=True)
+    training, momentum, eps = _bn_prepare(bn)
+    return _StemConvBN.apply(x.float(), conv.weight, bn.weight, bn.bias, bn.running_mean,
+                             bn.running_var, 2, conv.padding[0], training, momentum, eps)
+
+
 def conv_bn(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool,
             residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """z = act(BN(conv(x)) [+ residual]) on NHWC activations."""

@@ -444,3 +444,28 @@ def test_weight_mirror_matches_packs(gpu, native_ext):
     assert not sp.mirror().valid()
     ddp(x)
     check()
+
+
+def test_stem_superpixel_matches_generic(gpu, native_ext):
+    """Super-pixel stem (K = 224 implicit GEMM on a re-laid-out image) == channel-padded generic
+    stem (image_to_nhwc + conv_bn): forward output, running stats and parameter gradients."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(gpu)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    bn = torch.nn.BatchNorm2d(64).to(gpu)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(4, 3, 64, 96, device=gpu)
+    z1 = ops.stem_conv_bn(x, conv, bn)
+    z2 = ops.conv_bn(ops.image_to_nhwc(x), conv2, bn2, relu=True)
+    assert z1.shape == z2.shape == (4, 32, 48, 64)
+    assert _rel_err(z1, z2) < 1e-2
+    assert torch.allclose(bn.running_mean, bn2.running_mean, atol=1e-3, rtol=1e-2)
+    assert torch.allclose(bn.running_var, bn2.running_var, atol=1e-3, rtol=1e-2)
+    g = torch.randn(z1.shape, device=gpu).bfloat16()
+    z1.backward(g)
+    z2.backward(g)
+    assert _rel_err(conv.weight.grad, conv2.weight.grad) < 2e-2
+    assert _rel_err(bn.weight.grad, bn2.weight.grad) < 2e-2
+    assert _rel_err(bn.bias.grad, bn2.bias.grad) < 2e-2
