@@ -9,6 +9,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdexcept>
+
 namespace pdt {
 
 // ------------------------------------------------------------------ finalize
@@ -21,9 +23,49 @@ constexpr int FIN_CH = 32;
 constexpr int FIN_ROWS = 8;                 // threads per channel in a block
 constexpr int FIN_GPB = FIN_ROWS * 32;      // groups per block
 
-__global__ void __launch_bounds__(256) bn_finalize_stage1(const float* __restrict__ part, int ngroups,
+// Per-channel-tile completion counters for the single-launch two-level reductions below
+// (zero-initialised once; the last block of a tile resets its counter, so launches on one stream
+// can reuse them back to back).  Forward finalize uses [0, 2048), backward reduce [2048, 4096);
+// two launches of the SAME reduction must not run concurrently on different streams.
+constexpr int kTileCounters = 4096;
+__device__ unsigned int g_tile_counters[kTileCounters];
+
+// Last-arriver handshake (agent-scope release/acquire, MI355X_MICROARCH Guideline 16 pattern):
+// every block publishes its partial with plain stores; the block that completes tile `tile` last
+// gets true and may then read all partials of that tile with plain loads.
+__device__ __forceinline__ bool last_block_of_tile(int tile, unsigned int nblocks) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int prev = __hip_atomic_fetch_add(&g_tile_counters[tile], 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = prev == nblocks - 1;
+    if (last) {
+      __hip_atomic_store(&g_tile_counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// Stage 1 per block (32 channels x FIN_GPB groups) -> ws[p][3][K]; the last partition block of a
+// channel tile then sums the P partials in fixed order (deterministic) and writes mean, invstd,
+// scale, shift and the running-stat update: one launch per BatchNorm.
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int ngroups,
                                                           int grows, int M, int K,
-                                                          float* __restrict__ ws) {
+                                                          float* __restrict__ ws,
+                                                          float* __restrict__ rm,
+                                                          float* __restrict__ rv,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
+                                                          float momentum, float eps,
+                                                          float* __restrict__ out) {
   __shared__ float sS[FIN_ROWS][FIN_CH + 1], sA[FIN_ROWS][FIN_CH + 1], sB[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
@@ -48,33 +90,29 @@ __global__ void __launch_bounds__(256) bn_finalize_stage1(const float* __restric
     float* o = ws + ((int64_t)blockIdx.y * 3) * K;
     o[k] = S; o[K + k] = A; o[2 * K + k] = B;
   }
-}
-
-__global__ void __launch_bounds__(256) bn_finalize_stage2(const float* __restrict__ ws, int P, int M,
-                                                          int K, float* __restrict__ rm,
-                                                          float* __restrict__ rv,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta,
-                                                          float momentum, float eps,
-                                                          float* __restrict__ out) {
-  int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  float S = 0.f, A = 0.f, B = 0.f;
-#pragma unroll 4
-  for (int p = 0; p < P; ++p) {
-    const float* o = ws + ((int64_t)p * 3) * K;
-    S += o[k]; A += o[K + k]; B += o[2 * K + k];
+  if (!last_block_of_tile(blockIdx.x, gridDim.y)) return;
+  const int P = gridDim.y;
+  S = 0.f; A = 0.f; B = 0.f;
+  if (k < K) {
+    for (int p = ty; p < P; p += FIN_ROWS) {
+      const float* o = ws + ((int64_t)p * 3) * K;
+      S += o[k]; A += o[K + k]; B += o[2 * K + k];
+    }
   }
+  sS[ty][tx] = S; sA[ty][tx] = A; sB[ty][tx] = B;
+  __syncthreads();
+  if (ty != 0 || k >= K) return;
+  for (int r = 1; r < FIN_ROWS; ++r) { S += sS[r][tx]; A += sA[r][tx]; B += sB[r][tx]; }
   const float mu = S / (float)M;
   const float m2 = fmaxf(A + B - S * mu, 0.f);
-  float var = m2 / (float)M;
-  float invstd = rsqrtf(var + eps);
+  const float var = m2 / (float)M;
+  const float invstd = rsqrtf(var + eps);
   if (rm != nullptr) {
-    float unb = M > 1 ? m2 / (float)(M - 1) : var;
+    const float unb = M > 1 ? m2 / (float)(M - 1) : var;
     rm[k] = (1.f - momentum) * rm[k] + momentum * mu;
     rv[k] = (1.f - momentum) * rv[k] + momentum * unb;
   }
-  float sc = gamma[k] * invstd;
+  const float sc = gamma[k] * invstd;
   out[k] = mu;
   out[K + k] = invstd;
   out[2 * K + k] = sc;
@@ -89,10 +127,9 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
   // workspace for stage-1 partials lives after out[4][K] (caller allocates 4K + 3K*P floats)
   int P = ceil_div(ngroups, FIN_GPB);
   float* ws = out + 4 * (int64_t)K;
-  hipLaunchKernelGGL(bn_finalize_stage1, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
-                     ngroups, grows, M, K, ws);
-  hipLaunchKernelGGL(bn_finalize_stage2, dim3(ceil_div(K, 256)), dim3(256), 0, st, ws, P, M, K, rm,
-                     rv, gamma, beta, momentum, eps, out);
+  if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn_finalize: too many channels");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
+                     ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out);
 }
 
 __global__ void bn_eval_params_kernel(const float* rm, const float* rv, const float* gamma,
@@ -281,10 +318,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restr
   }
 }
 
-// stage 1 for partials produced by a BN-fused dgrad: block (32 channels, FIN_GPB groups),
-// fixed summation order -> ws[P][2][K] in the layout bn_bwd_reduce_stage2 consumes
-__global__ void __launch_bounds__(256) bn_bwd_part_stage1(const float* __restrict__ part, int G, int K,
-                                                          float* __restrict__ ws) {
+// Partials produced by a BN-fused dgrad: block (32 channels, FIN_GPB groups) sums its groups
+// into ws[p][2][K]; the last partition block of a channel tile sums the P partials (fixed order)
+// into sums[2][K] and optionally dgamma += b*invstd, dbeta += a.  One launch.
+__global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restrict__ part, int G, int K,
+                                                          float* __restrict__ ws,
+                                                          float* __restrict__ sums,
+                                                          const float* __restrict__ invstd,
+                                                          float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta) {
   __shared__ float sa[FIN_ROWS][FIN_CH + 1], sb[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
@@ -306,6 +348,26 @@ __global__ void __launch_bounds__(256) bn_bwd_part_stage1(const float* __restric
     float* o = ws + (int64_t)blockIdx.y * 2 * K;
     o[k] = a;
     o[K + k] = b;
+  }
+  if (!last_block_of_tile(kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
+  const int P = gridDim.y;
+  a = 0.f; b = 0.f;
+  if (k < K) {
+    for (int p = ty; p < P; p += FIN_ROWS) {
+      a += ws[(int64_t)p * 2 * K + k];
+      b += ws[(int64_t)p * 2 * K + K + k];
+    }
+  }
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty != 0 || k >= K) return;
+  for (int r = 1; r < FIN_ROWS; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
+  sums[k] = a;
+  sums[K + k] = b;
+  if (dgamma != nullptr) {
+    dgamma[k] += b * invstd[k];
+    dbeta[k] += a;
   }
 }
 
@@ -406,9 +468,9 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
 void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float* sums,
                                const float* invstd, float* dgamma, float* dbeta, hipStream_t st) {
   const int P = ceil_div(G, FIN_GPB);
-  hipLaunchKernelGGL(bn_bwd_part_stage1, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws);
-  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, P, K, sums,
-                     invstd, dgamma, dbeta);
+  if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn reduce: too many channels");
+  hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
+                     sums, invstd, dgamma, dbeta);
 }
 
 }  // namespace pdt
