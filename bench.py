@@ -48,6 +48,8 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--json-out", default=None)
+    p.add_argument("--graph", action="store_true",
+                   help="capture the whole training step in a HIP graph and replay it (native impl)")
     p.add_argument("--cudnn-benchmark", action="store_true",
                    help="stock path: let MIOpen search for the fastest conv solutions")
     return p.parse_args(argv)
@@ -124,6 +126,11 @@ def main(argv=None) -> int:
         opt.step()
         return loss
 
+    if args.graph:
+        from pytorch_distributed_tutorials_amd.utils.graph import CapturedStep
+        eager_step = step
+        step = CapturedStep(eager_step, warmup=max(1, min(args.warmup, 3)))
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -165,7 +172,7 @@ def main(argv=None) -> int:
                        "seq_len": None, "image_size": args.image_size,
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype,
-                       "cudnn_benchmark": bool(args.cudnn_benchmark),
+                       "cudnn_benchmark": bool(args.cudnn_benchmark), "graph": bool(args.graph),
                        "final_loss": round(final_loss, 4)},
         }
         line = json.dumps(res)

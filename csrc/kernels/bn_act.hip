@@ -9,6 +9,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace pdt {
@@ -29,6 +30,16 @@ constexpr int FIN_GPB = FIN_ROWS * 32;      // groups per block
 // two launches of the SAME reduction must not run concurrently on different streams.
 constexpr int kTileCounters = 4096;
 __device__ unsigned int g_tile_counters[kTileCounters];
+
+// PDT_BN_LASTBLOCK=0: two launches (partials, then finalize) instead of the last-block handshake
+static bool bn_lastblock() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_BN_LASTBLOCK");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
 
 // Last-arriver handshake (agent-scope release/acquire, MI355X_MICROARCH Guideline 16 pattern):
 // every block publishes its partial with plain stores; the block that completes tile `tile` last
@@ -65,13 +76,16 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta,
                                                           float momentum, float eps,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, int mode,
+                                                          int nparts) {
+  // mode 0: partials + last-block finalize (one launch); 1: partials only; 2: finalize only
   __shared__ float sS[FIN_ROWS][FIN_CH + 1], sA[FIN_ROWS][FIN_CH + 1], sB[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
   const int g0 = blockIdx.y * FIN_GPB;
   const int g1 = min(ngroups, g0 + FIN_GPB);
   float S = 0.f, A = 0.f, B = 0.f;
+  if (mode != 2) {
   if (k < K) {
 #pragma unroll 4
     for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
@@ -90,8 +104,10 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
     float* o = ws + ((int64_t)blockIdx.y * 3) * K;
     o[k] = S; o[K + k] = A; o[2 * K + k] = B;
   }
+  if (mode == 1) return;
   if (!last_block_of_tile(blockIdx.x, gridDim.y)) return;
-  const int P = gridDim.y;
+  }
+  const int P = mode == 2 ? nparts : gridDim.y;
   S = 0.f; A = 0.f; B = 0.f;
   if (k < K) {
     for (int p = ty; p < P; p += FIN_ROWS) {
@@ -128,8 +144,15 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
   int P = ceil_div(ngroups, FIN_GPB);
   float* ws = out + 4 * (int64_t)K;
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn_finalize: too many channels");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
-                     ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out);
+  if (bn_lastblock()) {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 0, P);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part,
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 2, P);
+  }
 }
 
 __global__ void bn_eval_params_kernel(const float* rm, const float* rv, const float* gamma,
@@ -326,13 +349,15 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
                                                           float* __restrict__ sums,
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta) {
+                                                          float* __restrict__ dbeta, int mode,
+                                                          int nparts) {
   __shared__ float sa[FIN_ROWS][FIN_CH + 1], sb[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
   const int g0 = blockIdx.y * FIN_GPB;
   const int g1 = min(G, g0 + FIN_GPB);
   float a = 0.f, b = 0.f;
+  if (mode != 2) {
   if (k < K) {
 #pragma unroll 4
     for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
@@ -349,8 +374,10 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
     o[k] = a;
     o[K + k] = b;
   }
+  if (mode == 1) return;
   if (!last_block_of_tile(kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
-  const int P = gridDim.y;
+  }
+  const int P = mode == 2 ? nparts : gridDim.y;
   a = 0.f; b = 0.f;
   if (k < K) {
     for (int p = ty; p < P; p += FIN_ROWS) {
@@ -469,8 +496,15 @@ void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float
                                const float* invstd, float* dgamma, float* dbeta, hipStream_t st) {
   const int P = ceil_div(G, FIN_GPB);
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn reduce: too many channels");
-  hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                     sums, invstd, dgamma, dbeta);
+  if (bn_lastblock()) {
+    hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
+                       sums, invstd, dgamma, dbeta, 0, P);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
+                       sums, invstd, dgamma, dbeta, 1, P);
+    hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part, G, K, ws,
+                       sums, invstd, dgamma, dbeta, 2, P);
+  }
 }
 
 }  // namespace pdt

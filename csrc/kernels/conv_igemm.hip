@@ -968,7 +968,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.div_w = make_fastdiv((uint32_t)s.Wo);
   a.steps_per_split = p.steps_per_split;
   a.nsteps = p.nsteps;
-  a.accumulate = accumulate ? 1 : 0;
+  a.accumulate = (accumulate && !slab) ? 1 : 0;  // slabs are private partials: always overwritten
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;

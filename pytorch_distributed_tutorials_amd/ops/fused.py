@@ -15,6 +15,7 @@ dgrad and wgrad implicit GEMMs.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -26,6 +27,20 @@ from ..utils.seed import deterministic
 from ._ext import native
 
 _CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
+# debugging switches for the fused backward (default on): BN backward inside the dgrad epilogue,
+# and its cross-block handoff
+_FUSE_DGRAD_BN = os.environ.get("PDT_DGRAD_BN", "1") != "0"
+_BN_HANDOFF = os.environ.get("PDT_BN_HANDOFF", "1") != "0"
+_NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
+
+
+def _nan_trace(tag, **tensors):
+    if not _NAN_TRACE:
+        return
+    torch.cuda.synchronize()
+    bad = [k for k, t in tensors.items() if t is not None and t.is_floating_point() and bool(torch.isnan(t).any())]
+    if bad:
+        print(f"[nan-trace] {tag}: NaN in {bad}", flush=True)
 
 
 def set_cpu_activation_dtype(dtype: torch.dtype) -> None:
@@ -147,6 +162,7 @@ class _StemConvBN(torch.autograd.Function):
         else:
             stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
         z = C.bn_act_fwd(y, stats[2], stats[3], None, True)
+        _nan_trace("stem", x=x, xsp=xsp, y=y, part=part, stats=stats, z=z)
         ctx.save_for_backward(xsp, y, stats, gamma)
         ctx.weight = weight
         ctx.training = training
@@ -210,6 +226,7 @@ class _MaxPool(torch.autograd.Function):
     def forward(ctx, x):
         if x.is_cuda:
             y, idx = native().maxpool_fwd(x)       # idx: argmax position 0..8 per output (uint8)
+            _nan_trace("maxpool", x=x, y=y)
             ctx.save_for_backward(idx)
         else:
             y = ref.maxpool3x3s2_fwd(x)
@@ -342,6 +359,10 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
     wk = _packed_krsc(C, w, cx)
     y, part = C.conv_fwd(x, wk, stride, pad, training)
+    if _NAN_TRACE:
+        m = _mirror_of(w)
+        _nan_trace(f"unit_fwd {tuple(x.shape)}->{tuple(y.shape)} mirror={m is not None and m.krsc_view(w) is wk}",
+                   x=x, wk=wk, y=y, part=part)
     if training:
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:
@@ -380,6 +401,7 @@ class _ResidualBlock(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, spec, handoff, *tensors):
         C = native()
+        _nan_trace(f"block-in {tuple(x.shape)}", x=x)
         chain, ds_cfg = spec
         nch = len(chain)
         saved = [x]
@@ -399,8 +421,9 @@ class _ResidualBlock(torch.autograd.Function):
                                   res if last else None)
             outs.append((z, y, stt))
             h = z
-        for z, y, stt in outs:
+        for ui, (z, y, stt) in enumerate(outs):
             saved += [z, y, stt]
+            _nan_trace(f"fwd block{id(ctx) % 10007} unit{ui} {tuple(y.shape)}", z=z, y=y, stats=stt)
         if ds_cfg is not None:
             saved += [y_ds, st_ds]
         ctx.save_for_backward(*saved, *tensors)
@@ -426,6 +449,10 @@ class _ResidualBlock(torch.autograd.Function):
             y_ds, st_ds = sv[pos:pos + 2]
             pos += 2
         tensors = sv[pos:]
+        if _NAN_TRACE:
+            for ui, (z_, y_, s_) in enumerate(units):
+                _nan_trace(f"bwd-entry block{id(ctx) % 10007} unit{ui} {tuple(y_.shape)}", z=z_, y=y_, stats=s_)
+            _nan_trace(f"bwd-entry block{id(ctx) % 10007} dz", dz=dz)
         grads = [None] * ctx.ntensors
         dz = dz.contiguous()
         det = deterministic()
@@ -512,7 +539,10 @@ class _ResidualBlock(torch.autograd.Function):
                 g_short = dres
             if i > 0:
                 yp, sttp = units[i - 1][1], units[i - 1][2]
-                pre = dgrad_bn(5 * (i - 1), dy, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
+                if _FUSE_DGRAD_BN:
+                    pre = dgrad_bn(5 * (i - 1), dy, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
+                else:
+                    dz = C.conv_dgrad(dy, w, list(xin.shape), st, pd, wt=_packed_crsk(w))
             else:
                 # shortcut gradient: identity -> g_short itself; projection -> its dgrad
                 if ds_cfg is not None:
@@ -531,7 +561,7 @@ class _ResidualBlock(torch.autograd.Function):
                     hi = ctx.handoff_in
                     sg = _grad_sink(hi.gamma) if hi is not None else None
                     sb = _grad_sink(hi.beta) if hi is not None else None
-                    if sg is not None and sb is not None and x.shape[3] % 8 == 0:
+                    if sg is not None and sb is not None and _BN_HANDOFF and _FUSE_DGRAD_BN:
                         # previous block's last unit: relu mask from its output z = x
                         dz, sums_in = C.conv_dgrad_bn(dy, w, list(x.shape), st, pd, addend, hi.y, x,
                                                       hi.stats, 1, sg, sb, _packed_crsk(w))

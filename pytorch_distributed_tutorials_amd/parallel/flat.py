@@ -12,6 +12,7 @@ bucket order.  Consequences:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -98,7 +99,8 @@ class FlatParamSpace:
 
     def mirror(self) -> "Optional[WeightMirror]":
         """bf16 conv-weight mirror (GPU spaces only), created on first use."""
-        if self._mirror is None and self.param_flat.is_cuda:
+        if self._mirror is None and self.param_flat.is_cuda \
+                and os.environ.get("PDT_WEIGHT_MIRROR", "1") != "0":
             self._mirror = WeightMirror(self)
         return self._mirror
 
