@@ -50,6 +50,8 @@ def parse(argv=None):
     p.add_argument("--json-out", default=None)
     p.add_argument("--graph", action="store_true",
                    help="capture the whole training step in a HIP graph and replay it (native impl)")
+    p.add_argument("--fp8", action="store_true",
+                   help="native impl: forward convs on the fp8 (e4m3) MX-rate MFMA, delayed scaling")
     p.add_argument("--cudnn-benchmark", action="store_true",
                    help="stock path: let MIOpen search for the fastest conv solutions")
     return p.parse_args(argv)
@@ -85,6 +87,10 @@ def main(argv=None) -> int:
     dev = torch.device(f"cuda:{env.local_rank}" if torch.cuda.is_available() else "cpu")
     torch.manual_seed(0)
 
+    if args.fp8:
+        if args.impl != "native" or args.graph:
+            raise SystemExit("--fp8 needs --impl native and no --graph (delayed scaling slots advance per call)")
+        ops.set_fp8(True)
     if args.impl == "native":
         model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
         model.set_impl("native")
@@ -153,10 +159,11 @@ def main(argv=None) -> int:
 
     if env.rank == 0:
         img_s = world * args.batch * args.steps / elapsed
-        base = STOCK_BASELINE_IMG_S.get(world)
+        base = STOCK_BASELINE_IMG_S.get(world) if args.arch == "resnet50" else None
         res = {
             "metric": "images/sec (whole node) ResNet-50 bf16 at 1/2/4/8 MI355X"
-            if args.arch == "resnet50" else f"images/sec (whole node) {args.arch} bf16",
+            if args.arch == "resnet50" and not args.fp8
+            else f"images/sec (whole node) {args.arch} {'fp8' if args.fp8 else 'bf16'}",
             "value": round(img_s, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -166,7 +173,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(img_s / base, 4) if base else None),
-            "dtype": "bf16",
+            "dtype": "fp8" if args.fp8 else "bf16",
             "data": "synthetic (ImageNet-shaped 3x224x224 fp32 images, random labels, random-init weights)",
             "config": {"model": args.arch, "global_batch": args.batch * world,
                        "seq_len": None, "image_size": args.image_size,

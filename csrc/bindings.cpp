@@ -563,6 +563,113 @@ void pack_t_batched(const Tensor& src, Tensor dst, const Tensor& table, int64_t 
 
 int64_t pack_t_entry_bytes() { return (int64_t)pdt::pack_t_entry_bytes(); }
 
+// ------------------------------------------------------------------- fp8
+void check_state(const Tensor& st, int64_t slot) {
+  check_cuda(st, "fp8 state");
+  TORCH_CHECK(st.scalar_type() == at::kFloat && st.numel() == 6, "fp8 state must be fp32 [6]");
+  TORCH_CHECK(slot >= 0 && slot < 3, "fp8 slot must be 0..2");
+}
+
+void check_u8_nhwc(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kByte && t.dim() == 4, name, " must be uint8 (fp8 bits) NHWC");
+  TORCH_CHECK(t.size(3) % 16 == 0, name, " channels must be a multiple of 16");
+  TORCH_CHECK(t.numel() < (int64_t(1) << 31), name, " too large for 32-bit buffer addressing");
+}
+
+// (wq uint8 e4m3 [K,R,S,Cp], oscale fp32 [K]); act_deq: optional 1-element dequant factor of the
+// activation operand, folded into oscale
+std::tuple<Tensor, Tensor> pack_weight_fp8(const Tensor& w, int64_t cpad, const std::optional<Tensor>& act_deq) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kFloat, "weight must be fp32 4-D");
+  c10::hip::HIPGuard g(w.get_device());
+  int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  int Cp = std::max<int>((int)cpad, C);
+  auto wq = at::empty({K, R, S, Cp}, w.options().dtype(at::kByte));
+  auto osc = at::empty({K}, w.options());
+  const float* ad = nullptr;
+  if (act_deq.has_value() && act_deq->defined()) {
+    TORCH_CHECK(act_deq->is_cuda() && act_deq->scalar_type() == at::kFloat && act_deq->numel() >= 1,
+                "act_deq must be a device fp32 scalar");
+    ad = act_deq->data_ptr<float>();
+  }
+  int64_t st[4] = {w.stride(0), w.stride(1), w.stride(2), w.stride(3)};
+  pdt::launch_pack_weight_fp8(w.data_ptr<float>(), st, wq.data_ptr<uint8_t>(), osc.data_ptr<float>(), ad, K,
+                              C, R, S, Cp, cur_stream(w));
+  return {wq, osc};
+}
+
+Tensor quant_e4m3(const Tensor& x, Tensor state, int64_t slot) {
+  check_bf16_nhwc(x, "x");
+  check_state(state, slot);
+  c10::hip::HIPGuard g(x.get_device());
+  auto q = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  pdt::launch_quant_e4m3(cbf(x), q.data_ptr<uint8_t>(), x.numel(), state.data_ptr<float>(), (int)slot,
+                         cur_stream(x));
+  return q;
+}
+
+std::tuple<Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, const Tensor& shift,
+                                         const std::optional<Tensor>& res, bool relu, Tensor state,
+                                         int64_t slot) {
+  check_bf16_nhwc(y, "y");
+  check_state(state, slot);
+  c10::hip::HIPGuard g(y.get_device());
+  int K = y.size(3);
+  int64_t M = y.numel() / K;
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_nhwc(*res, "residual");
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
+    rp = cbf(*res);
+  }
+  auto z = at::empty_like(y);
+  auto q = at::empty(y.sizes(), y.options().dtype(at::kByte));
+  pdt::launch_bn_act_fwd_q8(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z),
+                            q.data_ptr<uint8_t>(), M, K, state.data_ptr<float>(), (int)slot, cur_stream(y));
+  return {z, q};
+}
+
+std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const Tensor& oscale,
+                                        int64_t stride, int64_t pad, bool stats) {
+  check_u8_nhwc(x, "x");
+  check_cuda(wq, "wq");
+  TORCH_CHECK(wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(3) == x.size(3),
+              "packed fp8 weight must be uint8 [K,R,S,Cx]");
+  TORCH_CHECK(oscale.is_cuda() && oscale.scalar_type() == at::kFloat && oscale.numel() == wq.size(0),
+              "oscale must be fp32 [K]");
+  c10::hip::HIPGuard g(x.get_device());
+  auto s = shape_of(x.size(0), x.size(1), x.size(2), x.size(3), wq.size(0), wq.size(1), wq.size(2),
+                    stride, pad);
+  TORCH_CHECK(s.K % 8 == 0, "output channels must be a multiple of 8");
+  auto y = at::empty({s.N, s.Ho, s.Wo, s.K}, x.options().dtype(at::kBFloat16));
+  Tensor part;
+  float* pp = nullptr;
+  int M = s.N * s.Ho * s.Wo;
+  if (stats) {
+    int grows = pdt::conv_fwd_group_rows(M, s.K);
+    part = at::empty({(M + grows - 1) / grows, 2, s.K}, x.options().dtype(at::kFloat));
+    pp = part.data_ptr<float>();
+  }
+  pdt::launch_conv_fwd_fp8(x.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), oscale.data_ptr<float>(), bf(y),
+                           pp, s, cur_stream(x));
+  return {y, part};
+}
+
+// a, b: uint8 [64, 32] per-lane operand registers; returns fp32 [64, 4] accumulators
+Tensor mfma_f8_probe(const Tensor& a, const Tensor& b, int64_t fmt_a, int64_t fmt_b, int64_t scale_a,
+                     int64_t scale_b, bool use_scale) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kByte && b.scalar_type() == at::kByte && a.numel() == 64 * 32 &&
+              b.numel() == 64 * 32, "probe operands: uint8 [64, 32]");
+  TORCH_CHECK((fmt_a == 0 || fmt_a == 1) && (fmt_b == 0 || fmt_b == 1), "fmt: 0 = e4m3, 1 = e5m2");
+  c10::hip::HIPGuard g(a.get_device());
+  auto d = at::empty({64, 4}, a.options().dtype(at::kFloat));
+  pdt::launch_mfma_f8_probe(a.data_ptr(), b.data_ptr(), d.data_ptr<float>(), (int)fmt_a, (int)fmt_b,
+                            (int)scale_a, (int)scale_b, use_scale ? 1 : 0, cur_stream(a));
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -603,6 +710,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_to_bf16", checked("cast_to_bf16", &cast_to_bf16));
   m.def("pack_t_batched", checked("pack_t_batched", &pack_t_batched));
   m.def("pack_t_entry_bytes", &pack_t_entry_bytes);
+  m.def("pack_weight_fp8", checked("pack_weight_fp8", &pack_weight_fp8), py::arg("w"), py::arg("cpad") = 0,
+        py::arg("act_deq") = py::none());
+  m.def("quant_e4m3", checked("quant_e4m3", &quant_e4m3));
+  m.def("bn_act_fwd_q8", checked("bn_act_fwd_q8", &bn_act_fwd_q8), py::arg("y"), py::arg("scale"),
+        py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"));
+  m.def("conv_fwd_fp8", checked("conv_fwd_fp8", &conv_fwd_fp8), py::arg("x"), py::arg("wq"), py::arg("oscale"),
+        py::arg("stride"), py::arg("pad"), py::arg("stats"));
+  m.def("mfma_f8_probe", checked("mfma_f8_probe", &mfma_f8_probe), py::arg("a"), py::arg("b"),
+        py::arg("fmt_a") = 0, py::arg("fmt_b") = 0, py::arg("scale_a") = 127, py::arg("scale_b") = 127,
+        py::arg("use_scale") = true);
   m.def("conv_fwd_group_rows", &pdt::conv_fwd_group_rows);
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });

@@ -92,6 +92,14 @@ struct ReducerState {
                              average ? ncclAvg : ncclSum);
       }
     } else {
+      if (aux) {
+        // device gradients through a non-RCCL group (gloo on GPU tensors): the collective runs
+        // behind the caller's stream, so that stream joins the side stream first
+        const int dev = params[0].get_device();
+        c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
+        hipEventRecord(ev_aux, aux);
+        hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream(), ev_aux, 0);
+      }
       py::gil_scoped_acquire gil;
       py_launch(b);
     }
@@ -250,9 +258,10 @@ void Reducer::set_strict(bool on) { st_->strict = on; }
 
 void Reducer::set_aux_stream(uintptr_t stream) {
   std::lock_guard<std::mutex> lk(st_->mu);
-  if (!st_->comm) throw std::runtime_error("Reducer aux stream needs the RCCL communicator");
+  if (st_->params.empty() || !st_->params[0].is_cuda())
+    throw std::runtime_error("Reducer aux stream needs device parameters");
   if (!st_->ev_aux) {
-    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->comm->device());
+    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->params[0].get_device());
     if (hipEventCreateWithFlags(&st_->ev_aux, hipEventDisableTiming) != hipSuccess)
       throw std::runtime_error("hipEventCreate failed");
   }

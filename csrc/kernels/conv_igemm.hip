@@ -78,6 +78,24 @@ __device__ __forceinline__ v4f mfma16(const v4i& a, const v4i& b, const v4f& c) 
 
 constexpr uint32_t OOB = 0x80000000u;  // any offset >= num_records reads 0
 
+// Operand element type of the NT kernel: bf16, or fp8 with the activation operand in e4m3
+// (forward) or e5m2 (gradients); weights are always e4m3.  A K-step moves 128 bytes of every
+// operand row either way: 64 bf16 (two 16x16x32 MFMAs) or 128 fp8 (one MX-rate 16x16x128 MFMA,
+// twice the bf16 FLOP per cycle).  Offsets below are element offsets scaled by EB bytes.
+constexpr int OP_BF16 = 0;
+constexpr int OP_F8_E4M3 = 1;
+constexpr int OP_F8_E5M2 = 2;
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+// D += W(16 x 128, e4m3) * X(128 x 16, fmt XF), unit E8M0 block scales (the literal 0 operands
+// select the unscaled encoding: tests/test_fp8_gpu.py).  Lane l: row/col l&15, k bytes
+// 32*(l>>4) .. +31 -- identical for both operands, which is all the product needs.
+template <int XF>
+__device__ __forceinline__ v4f mfma_f8(const v8i& w, const v8i& x, const v4f& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, c, 0, XF == OP_F8_E5M2 ? 1 : 0, 0, 0, 0, 0);
+}
+
 // ============================================================================
 //                          NT implicit GEMM (fwd / dgrad)
 // ============================================================================
@@ -87,6 +105,7 @@ struct NtArgs {
   uint16_t* out;       // NHWC output, Nout channels
   const uint16_t* addend;  // optional NHWC tensor (same layout as out) added in the epilogue
   float* part;         // BN partials [ngroups][2][Nout] or null
+  const float* oscale; // fp8 operands: per-output-column dequantization factor (acc * oscale[col])
   uint32_t a_bytes, b_bytes;
   int HA, WA, CA;      // A source dims
   int Nout, Kg, S;     // GEMM N, B row length (= taps_total*CA), filter width (generic path)
@@ -175,10 +194,13 @@ __device__ __forceinline__ void wait_steps(int younger) {
 // MFMA operands are swapped (A = weights, B = pixels) so each lane's 4 accumulator registers are
 // 4 consecutive output channels of one pixel: the epilogue packs them into one 8-byte LDS write
 // and the BN statistics reduce over the 16 pixel-lanes with DPP-friendly xor shuffles.
-template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16>
 __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) {
   using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
+  constexpr int EB = OP == OP_BF16 ? 2 : 1;  // bytes per element
+  constexpr int KE = 128 / EB;               // elements per K-step (one 128-byte row)
+  constexpr int CE = 16 / EB;                // elements per 16-byte chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Nout + BN - 1) / BN;
@@ -214,7 +236,7 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     } else {
       a_pix[i] = 0; a_h0[i] = -(1 << 20); a_w0[i] = 0;
     }
-    a_base[i] = ((a_pix[i] + a_h0[i] * P.WA + a_w0[i]) * P.CA + a_c[i] * 8) * 2;
+    a_base[i] = (a_pix[i] + a_h0[i] * P.WA + a_w0[i]) * P.CA * EB + a_c[i] * 16;
   }
   int b_row[B_PW], b_c[B_PW];
 #pragma unroll
@@ -225,19 +247,19 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     b_row[i] = n < P.Nout ? n * P.Kg : -1;
   }
 
-  const int cb = P.CA >> 6;
-  const int nk = C64 ? P.ntaps * cb : (P.Kg + 63) / 64;
+  const int cb = P.CA / KE;  // 128-byte channel blocks per tap (C64 path)
+  const int nk = C64 ? P.ntaps * cb : (P.Kg + KE - 1) / KE;
 
   auto issue = [&](int kt, int buf) {
     char* As = smem + buf * (BM + BN) * 128;
     char* Bs = As + BM * 128;
     if constexpr (C64) {
       const int tap = kt / cb;
-      const int chb = (kt - tap * cb) * 64;
+      const int chb = (kt - tap * cb) * KE;
       const int ti = tap / P.tns, tj = tap - ti * P.tns;
       const int dr = P.dr0 + ti * P.dstep, ds = P.ds0 + tj * P.dstep;
       const int tbo = ((P.tr0 + ti * P.tstep) * P.S + (P.ts0 + tj * P.tstep)) * P.CA + chb;
-      const int tdelta = ((dr * P.WA + ds) * P.CA + chb) * 2;
+      const int tdelta = ((dr * P.WA + ds) * P.CA + chb) * EB;
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
         const int h = a_h0[i] + dr, w = a_w0[i] + ds;
@@ -247,26 +269,26 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       }
 #pragma unroll
       for (int i = 0; i < B_PW; ++i) {
-        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo + b_c[i] * 8) * 2) : OOB;
+        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * EB + b_c[i] * 16) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
-        const int kk = kt * 64 + a_c[i] * 8;
+        const int kk = kt * KE + a_c[i] * CE;
         const int tap = kk / P.CA;
         const int ch = kk - tap * P.CA;
         const int r = tap / P.S;
         const int s = tap - r * P.S;
         int h = a_h0[i] + r, w = a_w0[i] + s;
         bool ok = kk < P.Kg && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
-        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * 2) : OOB;
+        uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * EB) : OOB;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
       }
 #pragma unroll
       for (int i = 0; i < B_PW; ++i) {
-        const int kk = kt * 64 + b_c[i] * 8;
-        uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * 2) : OOB;
+        const int kk = kt * KE + b_c[i] * CE;
+        uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * EB) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     }
@@ -292,20 +314,43 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, nxt);
     const char* As = smem + cur * CFG::STAGE_BYTES;
     const char* Bs = As + BM * 128;
+    if constexpr (OP == OP_BF16) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int kc = ks * 4 + fq;
-      v4i af[TM], bfr[TN];
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kc = ks * 4 + fq;
+        v4i af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const v4i*>(As + swz128(wm * TM * 16 + i * 16 + fr, kc));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(wn * TN * 16 + j * 16 + fr, kc));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      }
+    } else {
+      // lane group fq owns bytes 32*fq .. +31 of the row = chunks 2fq, 2fq+1
+      v8i af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 16 + i * 16 + fr;
+        const v4i lo = *reinterpret_cast<const v4i*>(As + swz128(row, 2 * fq));
+        const v4i hi = *reinterpret_cast<const v4i*>(As + swz128(row, 2 * fq + 1));
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * TN * 16 + j * 16 + fr;
+        const v4i lo = *reinterpret_cast<const v4i*>(Bs + swz128(row, 2 * fq));
+        const v4i hi = *reinterpret_cast<const v4i*>(Bs + swz128(row, 2 * fq + 1));
+        bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const v4i*>(As + swz128(wm * TM * 16 + i * 16 + fr, kc));
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(wn * TN * 16 + j * 16 + fr, kc));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f8<OP>(bfr[j], af[i], acc[i][j]);
     }
     wait_steps<LPS>(min(nk - 1, kt + STAGES - 1) - (kt + 1));
     lds_barrier();
@@ -317,6 +362,20 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   // lane (fq, fr), register e of acc[i][j]: pixel i*16 + fr, channel j*16 + fq*4 + e
   const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
   const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
+
+  if constexpr (OP != OP_BF16) {
+    // fp8: back to real units with the per-column factor (weight scale x activation scale)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wcol0 + j * 16 + fq * 4;
+      const float4 sc = col < P.Nout ? *reinterpret_cast<const float4*>(P.oscale + col)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j][0] *= sc.x; acc[i][j][1] *= sc.y; acc[i][j][2] *= sc.z; acc[i][j][3] *= sc.w;
+      }
+    }
+  }
 
   if constexpr (EPI == EPI_STATS) {
     // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels;
@@ -724,12 +783,12 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16>
 static void run_nt(const NtArgs& a, hipStream_t st) {
   using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   int ntm = (a.M + CFG::BM - 1) / CFG::BM;
   int ntn = (a.Nout + CFG::BN - 1) / CFG::BN;
-  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, STAGES, C64, EPI>;
+  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, STAGES, C64, EPI, OP>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -737,7 +796,8 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
   }
   // a K loop shorter than the pipeline never touches the last buffers: request only the LDS it
   // uses so more blocks fit per CU (the short-K 1x1 convs are bound by their epilogue stores)
-  const int nk = C64 ? a.ntaps * (a.CA / 64) : (a.Kg + 63) / 64;
+  constexpr int KE = OP == OP_BF16 ? 64 : 128;
+  const int nk = C64 ? a.ntaps * (a.CA / KE) : (a.Kg + KE - 1) / KE;
   const int smem = std::max(std::max(1, std::min(nk, STAGES)) * CFG::STAGE_BYTES, CFG::EPI_BYTES);
   hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), smem, st, a);
   check_launch("igemm_nt");
@@ -772,26 +832,33 @@ static int nt_tile_mode() {
   return v;
 }
 
-static bool use_wide_tile(const NtArgs& a) {
+static bool use_wide_tile(const NtArgs& a, int kg_bytes) {
   const int mode = nt_tile_mode();
   if (mode == 1 || a.Nout < 256) return false;
   if (mode == 2) return true;
   const int64_t blocks = (int64_t)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
-  return a.Kg >= 128 && blocks >= 196;
+  return kg_bytes >= 256 && blocks >= 196;
 }
 
 // tile choice: output channels 64 -> tall tile (more M rows per block); small M -> short tile;
 // big GEMMs -> 256x256
-template <bool C64, int EPI>
+template <bool C64, int EPI, int OP = OP_BF16>
 static void dispatch_nt(const NtArgs& a, hipStream_t st, int* group_rows) {
   if (group_rows) *group_rows = (a.Nout > 64 && a.M <= 8192) ? 32 : 64;
+  if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
+    if (a.Nout <= 64) run_nt<4, 1, 4, 4, 2, C64, EPI, OP>(a, st);
+    else if (a.M <= 8192) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
+    else if (use_wide_tile(a, a.Kg)) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
+    else run_nt<2, 2, 4, 4, 2, C64, EPI, OP>(a, st);
+    return;
+  }
   if (a.Nout <= 64) {
     if (nt_stages(0) == 3) run_nt<4, 1, 4, 4, 3, C64, EPI>(a, st);  // 256 x 64
     else run_nt<4, 1, 4, 4, 2, C64, EPI>(a, st);
   } else if (a.M <= 8192) {
     if (nt_stages(1) == 3) run_nt<2, 2, 2, 4, 3, C64, EPI>(a, st);  // 64 x 128
     else run_nt<2, 2, 2, 4, 2, C64, EPI>(a, st);
-  } else if (use_wide_tile(a)) {
+  } else if (use_wide_tile(a, a.Kg * 2)) {
     run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);  // 256 x 256
   } else {
     if (nt_stages(2) == 3) run_nt<2, 2, 4, 4, 3, C64, EPI>(a, st);  // 128 x 128
@@ -831,6 +898,34 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   } else {
     if (c64) dispatch_nt<true, EPI_PLAIN>(a, st, nullptr);
     else dispatch_nt<false, EPI_PLAIN>(a, st, nullptr);
+  }
+}
+
+void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, uint16_t* y,
+                         float* part, const ConvShape& s, hipStream_t st) {
+  if (s.C % 16 != 0) throw std::runtime_error("conv_fwd_fp8: input channels must be a multiple of 16");
+  NtArgs a{};
+  a.a = reinterpret_cast<const uint16_t*>(x); a.b = reinterpret_cast<const uint16_t*>(w);
+  a.out = y; a.part = part; a.oscale = oscale;
+  a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C);
+  a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C);
+  a.HA = s.H; a.WA = s.W; a.CA = s.C;
+  a.Nout = s.K; a.Kg = s.R * s.S * s.C; a.S = s.S;
+  a.M = s.N * s.Ho * s.Wo;
+  fill_common(a, s.Ho, s.Wo);
+  a.ash = s.stride; a.asw = s.sw(); a.aoff_h = -s.pad; a.aoff_w = -s.pad;
+  a.OH = s.Ho; a.OW = s.Wo; a.osh = 1; a.osw = 1; a.oph = 0; a.opw = 0;
+  a.dense = 1;
+  a.tnr = s.R; a.tns = s.S; a.ntaps = s.R * s.S;
+  a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
+  a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
+  const bool c128 = (s.C % 128) == 0;
+  if (part) {
+    if (c128) dispatch_nt<true, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
+    else dispatch_nt<false, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
+  } else {
+    if (c128) dispatch_nt<true, EPI_PLAIN, OP_F8_E4M3>(a, st, nullptr);
+    else dispatch_nt<false, EPI_PLAIN, OP_F8_E4M3>(a, st, nullptr);
   }
 }
 

@@ -135,4 +135,27 @@ void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t st);
 
+// ----------------------------------------------------------------- fp8.hip
+// One v_mfma_scale_f32_16x16x128_f8f6f4 on raw per-lane operand registers (64 lanes x 32 bytes
+// each for A and B), D = 64 lanes x 4 fp32.  fmt 0 = e4m3, 1 = e5m2; scales are E8M0 bytes
+// (use_scale = 0 passes the literal 0 the way composable_kernel does).
+void launch_mfma_f8_probe(const void* a_regs, const void* b_regs, float* d, int fmt_a, int fmt_b,
+                          int scale_a, int scale_b, int use_scale, hipStream_t st);
+struct WStridesF8 { int64_t k, c, r, s; };
+// fp32 weight [K][C][R][S] (strides) -> e4m3 [K][R][S][Cp] with per-output-channel scale
+// ws_k = amax_k/448; oscale[k] = ws_k * act_deq[0] (act_deq may be null: 1) is the conv
+// epilogue's dequantization factor for column k.
+void launch_pack_weight_fp8(const float* w, const int64_t* strides, uint8_t* wq, float* oscale,
+                            const float* act_deq, int K, int C, int R, int S, int Cp, hipStream_t st);
+// Delayed-scaling state: float[6] = amax of the last 3 calls, then their dequant factors;
+// `slot` = call index % 3 (kept by the caller).  deq of this call lands in state[3 + slot].
+void launch_quant_e4m3(const uint16_t* x, uint8_t* q, int64_t n, float* state, int slot, hipStream_t st);
+// bn_act_fwd that also writes the e4m3 copy q of z (same delayed-scaling contract)
+void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* shift, const uint16_t* res,
+                          bool relu, uint16_t* z, uint8_t* q, int64_t M, int K, float* state, int slot,
+                          hipStream_t st);
+// fp8 forward conv: x e4m3 NHWC (C % 16 == 0), w e4m3 [K][R][S][C], y bf16 = (x*w) * oscale[k]
+void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, uint16_t* y,
+                         float* part, const ConvShape& s, hipStream_t st);
+
 }  // namespace pdt

@@ -192,6 +192,7 @@ class ResNet(nn.Module):
                 x = ops.image_to_nhwc(x)
             x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
         x = ops.maxpool3x3s2(x)
+        x = ops.fp8_attach(x, self.maxpool)  # e4m3 copy for fp8 convs (no-op unless ops.set_fp8)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 x = blk.forward_native(x)

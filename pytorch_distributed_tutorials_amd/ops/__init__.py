@@ -11,9 +11,12 @@ from .fused import (  # noqa: F401
     avgpool_linear,
     conv_bn,
     cross_entropy,
+    fp8_attach,
+    fp8_enabled,
     image_to_nhwc,
     maxpool3x3s2,
     residual_block,
+    set_fp8,
     set_cpu_activation_dtype,
     stem_conv_bn,
     top1_correct,

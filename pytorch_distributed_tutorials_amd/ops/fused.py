@@ -32,6 +32,54 @@ _CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
 _FUSE_DGRAD_BN = os.environ.get("PDT_DGRAD_BN", "1") != "0"
 _BN_HANDOFF = os.environ.get("PDT_BN_HANDOFF", "1") != "0"
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
+_FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
+
+
+def set_fp8(on: bool) -> None:
+    """fp8 forward convolutions: activations e4m3 with delayed per-tensor scaling (emitted by the
+    producing BatchNorm apply), weights e4m3 with per-output-channel scales, fp32 accumulation on
+    v_mfma_f32_16x16x128_f8f6f4, bf16 output; backward GEMMs stay bf16 on the saved bf16 tensors."""
+    global _FP8
+    _FP8 = bool(on)
+
+
+def fp8_enabled() -> bool:
+    return _FP8
+
+
+class _Q8State:
+    """Delayed-scaling state of one fp8 activation producer (csrc/kernels/fp8.hip contract)."""
+
+    __slots__ = ("buf", "t")
+
+    def __init__(self, device):
+        self.buf = torch.zeros(6, dtype=torch.float32, device=device)
+        self.t = 0
+
+    def next_slot(self) -> int:
+        slot = self.t % 3
+        self.t += 1
+        return slot
+
+    def deq(self, slot: int) -> torch.Tensor:
+        return self.buf.narrow(0, 3 + slot, 1)
+
+
+def _q8_state(owner: nn.Module, device) -> _Q8State:
+    st = getattr(owner, "_pdt_q8", None)
+    if st is None or st.buf.device != device:
+        st = _Q8State(device)
+        owner._pdt_q8 = st
+    return st
+
+
+def fp8_attach(x: torch.Tensor, owner: nn.Module) -> torch.Tensor:
+    """Attach an e4m3 copy of the NHWC activation ``x`` (for the fp8 convs that consume it)."""
+    if _FP8 and x.is_cuda and x.dim() == 4 and x.shape[3] % 16 == 0:
+        st = _q8_state(owner, x.device)
+        slot = st.next_slot()
+        x._pdt_fp8 = (native().quant_e4m3(x, st.buf, slot), st.deq(slot))
+    return x
 
 
 def _nan_trace(tag, **tensors):
@@ -353,12 +401,19 @@ def _packed_crsk(w):
     return m.crsk_view(w) if m is not None else None
 
 
-def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual):
+def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual,
+              x8=None, q8=None):
+    """conv -> BN -> (+residual) -> (ReLU).  x8 = (e4m3 copy of x, its dequant factor): fp8 conv;
+    q8 = _Q8State: also emit the e4m3 copy of the output (returned as the 4th value)."""
     k, _, r, s = w.shape
     n, h, wd, cx = x.shape
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
-    wk = _packed_krsc(C, w, cx)
-    y, part = C.conv_fwd(x, wk, stride, pad, training)
+    if x8 is not None:
+        wq, osc = C.pack_weight_fp8(w, cx, x8[1])
+        y, part = C.conv_fwd_fp8(x8[0], wq, osc, stride, pad, training)
+    else:
+        wk = _packed_krsc(C, w, cx)
+        y, part = C.conv_fwd(x, wk, stride, pad, training)
     if _NAN_TRACE:
         m = _mirror_of(w)
         _nan_trace(f"unit_fwd {tuple(x.shape)}->{tuple(y.shape)} mirror={m is not None and m.krsc_view(w) is wk}",
@@ -367,8 +422,12 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:
         stats = C.bn_eval_params(rm, rv, gamma, beta, float(eps))
+    if q8 is not None and k % 16 == 0:
+        slot = q8.next_slot()
+        z, zq = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot)
+        return z, y, stats, (zq, q8.deq(slot))
     z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu)
-    return z, y, stats
+    return z, y, stats, None
 
 
 class _BnHandoff:
@@ -399,28 +458,32 @@ class _ResidualBlock(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, spec, handoff, *tensors):
+    def forward(ctx, x, spec, handoff, fp8io, *tensors):
         C = native()
         _nan_trace(f"block-in {tuple(x.shape)}", x=x)
         chain, ds_cfg = spec
         nch = len(chain)
         saved = [x]
+        # fp8io = (x8, per-chain-unit _Q8State list, holder for the output's e4m3 copy) or None
+        x8, q8s, holder = fp8io if fp8io is not None else (None, None, None)
         # shortcut first (it only needs x) so its output can be freed into the tail's add
         if ds_cfg is not None:
             w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
             st, pd, tr, mo, ep = ds_cfg
-            res, y_ds, st_ds = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None)
+            res, y_ds, st_ds, _ = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None, x8)
         else:
             res = x
-        h = x
+        h, h8 = x, x8
         outs = []
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
             last = i == nch - 1
-            z, y, stt = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
-                                  res if last else None)
+            z, y, stt, h8 = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
+                                      res if last else None, h8, q8s[i] if q8s else None)
             outs.append((z, y, stt))
             h = z
+        if holder is not None and h8 is not None:
+            holder.append(h8)
         for ui, (z, y, stt) in enumerate(outs):
             saved += [z, y, stt]
             _nan_trace(f"fwd block{id(ctx) % 10007} unit{ui} {tuple(y.shape)}", z=z, y=y, stats=stt)
@@ -571,7 +634,7 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.handoff_in = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
-        return (dz, None, None, *grads)
+        return (dz, None, None, None, *grads)
 
 
 def _grad_sink(p):
@@ -596,9 +659,15 @@ def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
         tr, mo, ep = _bn_prepare(bn)
         ds_spec = (conv.stride[0], conv.padding[0], tr, mo, ep)
         tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    fp8io = None
+    if _FP8:
+        q8s = [_q8_state(bn, x.device) for _, bn in chain]
+        fp8io = (getattr(x, "_pdt_fp8", None), q8s, [])
     out = _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec), getattr(x, "_pdt_handoff", None),
-                               *tensors)
+                               fp8io, *tensors)
     node = out.grad_fn  # the ctx of this block's node (None without autograd)
     if node is not None and getattr(node, "handoff_out", None) is not None:
         out._pdt_handoff = node.handoff_out
+    if fp8io is not None and fp8io[2]:
+        out._pdt_fp8 = fp8io[2][0]
     return out

@@ -210,7 +210,7 @@ class DistributedDataParallel(nn.Module):
                                           self._py_launch, self._py_finalize)
             self._flats = flats
             self.space.reducer = self.reducer
-            if self.comm is not None:
+            if self.device.type == "cuda" and hasattr(self.reducer, "set_aux_stream"):
                 from ..ops import streams
                 side = streams.wgrad_stream(self.device)
                 if side is not None:  # weight gradients are produced on a side stream

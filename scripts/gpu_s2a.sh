@@ -1,0 +1,14 @@
+#!/bin/bash
+# Session-2 re-validation: GPU tests, smoke, eager + graph bench, rocprof kernel stats.
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R"; export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=$R/gpurun_out; mkdir -p $O
+ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
+step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc" | tee -a $O/status.txt; return $rc; }
+step pytest_s2a timeout -k 10 480 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread; ok $? || exit 1
+step smoke_s2a timeout -k 10 200 python __graft_entry__.py smoke || exit 1
+step bench_s2a timeout -k 10 300 python bench.py --steps 20 --warmup 5 || exit 1
+step bench_graph_s2a timeout -k 10 300 python bench.py --steps 20 --warmup 5 --graph || exit 1
+cd /tmp && export TMPDIR=/tmp
+step prof_s2a timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s2a -o run -- python3 $R/bench.py --steps 3 --warmup 2
+exit 0
