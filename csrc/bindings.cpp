@@ -73,6 +73,20 @@ void check_bf16_nhwc(const Tensor& t, const char* name) {
   TORCH_CHECK(t.numel() < (int64_t(1) << 30), name, " too large for 32-bit buffer addressing");
 }
 
+void check_state(const Tensor& st, int64_t slot) {
+  check_cuda(st, "fp8 state");
+  TORCH_CHECK(st.scalar_type() == at::kFloat && st.numel() == pdt::fp8_state_floats(),
+              "fp8 state must be fp32 [fp8_state_floats()]");
+  TORCH_CHECK(slot >= 0 && slot < 3, "fp8 slot must be 0..2");
+}
+
+void check_u8_nhwc(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kByte && t.dim() == 4, name, " must be uint8 (fp8 bits) NHWC");
+  TORCH_CHECK(t.size(3) % 16 == 0, name, " channels must be a multiple of 16");
+  TORCH_CHECK(t.numel() < (int64_t(1) << 31), name, " too large for 32-bit buffer addressing");
+}
+
 uint16_t* bf(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 const uint16_t* cbf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 
@@ -178,20 +192,15 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
 // returns (g, sums) with g = dx * relu'(unit) (mask 0/1/2 as bn_act_bwd_reduce) and
 // sums[2][C] = (sum g, sum g*(y - mean)); optional dgamma/dbeta accumulate like
 // bn_act_bwd_reduce.  bn_act_bwd_apply(g, ..., mask=0) then yields that unit's dy.
-std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs,
-                                         int64_t stride, int64_t pad,
+// shared body of conv_dgrad_bn / conv_dgrad_bn_fp8: `launch(s, dx, addend, bn, stream)` runs the
+// BN-fused dgrad
+template <typename Launch>
+std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvShape& s,
                                          const std::optional<Tensor>& addend, const Tensor& y,
-                                         const std::optional<Tensor>& z, const Tensor& stats,
-                                         int64_t mask, const std::optional<Tensor>& dgamma,
-                                         const std::optional<Tensor>& dbeta,
-                                         const std::optional<Tensor>& wt_in) {
-  check_bf16_nhwc(dy, "dy");
+                                         const std::optional<Tensor>& z, const Tensor& stats, int64_t mask,
+                                         const std::optional<Tensor>& dgamma,
+                                         const std::optional<Tensor>& dbeta, Launch&& launch) {
   check_bf16_nhwc(y, "y");
-  TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
-  TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
-  c10::hip::HIPGuard g(dy.get_device());
-  auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
-  TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
   TORCH_CHECK(y.size(0) == s.N && y.size(1) == s.H && y.size(2) == s.W && y.size(3) == s.C,
               "dgrad_bn: y must have the shape of x");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * s.C && stats.is_contiguous(),
@@ -204,8 +213,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
     TORCH_CHECK(z->sizes() == y.sizes(), "z shape mismatch");
     zp = cbf(*z);
   }
-  Tensor wt = packed_t_or_pack(w, wt_in);
-  auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
+  auto dx = at::empty({s.N, s.H, s.W, s.C}, y.options());
   const uint16_t* ap = nullptr;
   if (addend.has_value() && addend->defined()) {
     check_bf16_nhwc(*addend, "addend");
@@ -213,13 +221,13 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
     ap = cbf(*addend);
   }
   const int G = pdt::conv_dgrad_bn_groups(s);
-  auto fopt = dy.options().dtype(at::kFloat);
+  auto fopt = y.options().dtype(at::kFloat);
   auto part = at::empty({(int64_t)G * 2 * s.C}, fopt);
   auto ws = at::empty({(int64_t)pdt::bn_bwd_part_ws_floats(G, s.C)}, fopt);
   auto sums = at::empty({2, s.C}, fopt);
   pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
-  hipStream_t st = cur_stream(dy);
-  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, st, &bn);
+  hipStream_t st = cur_stream(dy_like);
+  launch(s, bf(dx), ap, &bn, st);
   float* dg = nullptr;
   float* db = nullptr;
   if (dgamma.has_value() && dgamma->defined()) {
@@ -232,6 +240,78 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
   pdt::launch_bn_bwd_part_reduce(part.data_ptr<float>(), G, s.C, ws.data_ptr<float>(),
                                  sums.data_ptr<float>(), stats.data_ptr<float>() + s.C, dg, db, st);
   return {dx, sums};
+}
+
+std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs,
+                                         int64_t stride, int64_t pad,
+                                         const std::optional<Tensor>& addend, const Tensor& y,
+                                         const std::optional<Tensor>& z, const Tensor& stats,
+                                         int64_t mask, const std::optional<Tensor>& dgamma,
+                                         const std::optional<Tensor>& dbeta,
+                                         const std::optional<Tensor>& wt_in) {
+  check_bf16_nhwc(dy, "dy");
+  TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
+  TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
+  c10::hip::HIPGuard g(dy.get_device());
+  auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
+  TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
+  Tensor wt = packed_t_or_pack(w, wt_in);
+  return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta,
+                       [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
+                           hipStream_t st) { pdt::launch_conv_dgrad(cbf(dy), cbf(wt), dx, ap, sh, st, bn); });
+}
+
+// fp8 dgrad operands: dy8 e5m2 NHWC [N,Ho,Wo,K], wt8 e4m3 [C,R,S,K] with per-C scale wscale,
+// dy dequant factor ascale (device scalar)
+pdt::ConvShape fp8_dgrad_shape(const Tensor& dy8, const Tensor& wt8, const Tensor& wscale, const Tensor& ascale,
+                               const std::vector<int64_t>& xs, int64_t stride, int64_t pad) {
+  check_u8_nhwc(dy8, "dy8");
+  check_cuda(wt8, "wt8");
+  TORCH_CHECK(wt8.scalar_type() == at::kByte && wt8.dim() == 4, "wt8 must be uint8 [C,R,S,K]");
+  TORCH_CHECK(xs.size() == 4 && xs[3] == wt8.size(0), "dgrad: x channels must equal weight in-channels");
+  TORCH_CHECK(wscale.is_cuda() && wscale.scalar_type() == at::kFloat && wscale.numel() == wt8.size(0),
+              "wscale must be fp32 [C]");
+  TORCH_CHECK(ascale.is_cuda() && ascale.scalar_type() == at::kFloat && ascale.numel() >= 1,
+              "ascale must be a device fp32 scalar");
+  auto s = shape_of(xs[0], xs[1], xs[2], xs[3], wt8.size(3), wt8.size(1), wt8.size(2), stride, pad);
+  TORCH_CHECK(s.Ho == dy8.size(1) && s.Wo == dy8.size(2) && s.K == dy8.size(3), "dgrad: dy shape mismatch");
+  TORCH_CHECK(s.K % 128 == 0, "fp8 dgrad: output channels must be a multiple of 128");
+  return s;
+}
+
+Tensor conv_dgrad_fp8(const Tensor& dy8, const Tensor& wt8, const Tensor& wscale, const Tensor& ascale,
+                      std::vector<int64_t> xs, int64_t stride, int64_t pad,
+                      const std::optional<Tensor>& addend) {
+  c10::hip::HIPGuard g(dy8.get_device());
+  auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
+  auto dx = at::empty({s.N, s.H, s.W, s.C}, dy8.options().dtype(at::kBFloat16));
+  const uint16_t* ap = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    check_bf16_nhwc(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    ap = cbf(*addend);
+  }
+  pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(), wscale.data_ptr<float>(),
+                             ascale.data_ptr<float>(), bf(dx), ap, s, cur_stream(dy8));
+  return dx;
+}
+
+std::tuple<Tensor, Tensor> conv_dgrad_bn_fp8(const Tensor& dy8, const Tensor& wt8, const Tensor& wscale,
+                                             const Tensor& ascale, std::vector<int64_t> xs, int64_t stride,
+                                             int64_t pad, const std::optional<Tensor>& addend,
+                                             const Tensor& y, const std::optional<Tensor>& z,
+                                             const Tensor& stats, int64_t mask,
+                                             const std::optional<Tensor>& dgamma,
+                                             const std::optional<Tensor>& dbeta) {
+  c10::hip::HIPGuard g(dy8.get_device());
+  auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
+  return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta,
+                       [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
+                           hipStream_t st) {
+                         pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(),
+                                                    wscale.data_ptr<float>(), ascale.data_ptr<float>(), dx,
+                                                    ap, sh, st, bn);
+                       });
 }
 
 // dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
@@ -443,6 +523,47 @@ std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, c
   return {dy, dres};
 }
 
+// (dy, dres, dy8): bn_act_bwd_apply (training) that also emits dy8 = e5m2(dy * s_t)
+std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const Tensor& z, const Tensor& y,
+                                                       const Tensor& stats, const Tensor& gamma,
+                                                       const Tensor& sums, int64_t mask, bool want_dres,
+                                                       Tensor state, int64_t slot) {
+  check_bf16_nhwc(dz, "dz");
+  check_bf16_nhwc(y, "y");
+  check_state(state, slot);
+  c10::hip::HIPGuard g(dz.get_device());
+  int K = y.size(3);
+  TORCH_CHECK(256 % (K / 8) == 0, "bn backward: channels must divide 2048 and be a power of two");
+  TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
+  if (mask == 1) check_bf16_nhwc(z, "z");
+  int64_t M = y.numel() / K;
+  auto dy = at::empty_like(dz);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(dz);
+  auto dy8 = at::empty(dz.sizes(), dz.options().dtype(at::kByte));
+  pdt::launch_bn_act_bwd_apply_q8(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
+                                  gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)mask, true, M, K,
+                                  bf(dy), want_dres ? bf(dres) : nullptr, dy8.data_ptr<uint8_t>(),
+                                  state.data_ptr<float>(), (int)slot, cur_stream(dz));
+  return {dy, dres, dy8};
+}
+
+// batched row-wise e4m3 quantization of a flat bf16 weight mirror (table: QRowEntry bytes)
+void quant_rows_e4m3(const Tensor& src, Tensor dst, Tensor scale, const Tensor& table, int64_t max_rows) {
+  check_cuda(src, "src");
+  check_cuda(dst, "dst");
+  check_cuda(scale, "scale");
+  TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kByte &&
+              scale.scalar_type() == at::kFloat && src.numel() == dst.numel(), "quant_rows: bf16 -> uint8");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kByte && table.is_contiguous(),
+              "quant_rows: table must be a device byte tensor");
+  const int64_t eb = (int64_t)pdt::quant_rows_entry_bytes();
+  TORCH_CHECK(table.numel() % eb == 0, "quant_rows: table size");
+  c10::hip::HIPGuard gd(src.get_device());
+  pdt::launch_quant_rows_e4m3(cbf(src), dst.data_ptr<uint8_t>(), scale.data_ptr<float>(), table.data_ptr(),
+                              (int)(table.numel() / eb), (int)max_rows, cur_stream(src));
+}
+
 // -------------------------------------------------------------------- pool
 std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x) {
   check_bf16_nhwc(x, "x");
@@ -564,19 +685,6 @@ void pack_t_batched(const Tensor& src, Tensor dst, const Tensor& table, int64_t 
 int64_t pack_t_entry_bytes() { return (int64_t)pdt::pack_t_entry_bytes(); }
 
 // ------------------------------------------------------------------- fp8
-void check_state(const Tensor& st, int64_t slot) {
-  check_cuda(st, "fp8 state");
-  TORCH_CHECK(st.scalar_type() == at::kFloat && st.numel() == 6, "fp8 state must be fp32 [6]");
-  TORCH_CHECK(slot >= 0 && slot < 3, "fp8 slot must be 0..2");
-}
-
-void check_u8_nhwc(const Tensor& t, const char* name) {
-  check_cuda(t, name);
-  TORCH_CHECK(t.scalar_type() == at::kByte && t.dim() == 4, name, " must be uint8 (fp8 bits) NHWC");
-  TORCH_CHECK(t.size(3) % 16 == 0, name, " channels must be a multiple of 16");
-  TORCH_CHECK(t.numel() < (int64_t(1) << 31), name, " too large for 32-bit buffer addressing");
-}
-
 // (wq uint8 e4m3 [K,R,S,Cp], oscale fp32 [K]); act_deq: optional 1-element dequant factor of the
 // activation operand, folded into oscale
 std::tuple<Tensor, Tensor> pack_weight_fp8(const Tensor& w, int64_t cpad, const std::optional<Tensor>& act_deq) {
@@ -630,7 +738,8 @@ std::tuple<Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, c
 }
 
 std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const Tensor& oscale,
-                                        int64_t stride, int64_t pad, bool stats) {
+                                        int64_t stride, int64_t pad, bool stats,
+                                        const std::optional<Tensor>& ascale) {
   check_u8_nhwc(x, "x");
   check_cuda(wq, "wq");
   TORCH_CHECK(wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(3) == x.size(3),
@@ -650,8 +759,14 @@ std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const
     part = at::empty({(M + grows - 1) / grows, 2, s.K}, x.options().dtype(at::kFloat));
     pp = part.data_ptr<float>();
   }
-  pdt::launch_conv_fwd_fp8(x.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), oscale.data_ptr<float>(), bf(y),
-                           pp, s, cur_stream(x));
+  const float* asp = nullptr;
+  if (ascale.has_value() && ascale->defined()) {
+    TORCH_CHECK(ascale->is_cuda() && ascale->scalar_type() == at::kFloat && ascale->numel() >= 1,
+                "ascale must be a device fp32 scalar");
+    asp = ascale->data_ptr<float>();
+  }
+  pdt::launch_conv_fwd_fp8(x.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), oscale.data_ptr<float>(), asp,
+                           bf(y), pp, s, cur_stream(x));
   return {y, part};
 }
 
@@ -713,10 +828,22 @@ PYBIND11_MODULE(_C, m) {
   m.def("pack_weight_fp8", checked("pack_weight_fp8", &pack_weight_fp8), py::arg("w"), py::arg("cpad") = 0,
         py::arg("act_deq") = py::none());
   m.def("quant_e4m3", checked("quant_e4m3", &quant_e4m3));
+  m.def("fp8_state_floats", &pdt::fp8_state_floats);
+  m.def("fp8_deq_offset", &pdt::fp8_deq_offset);
   m.def("bn_act_fwd_q8", checked("bn_act_fwd_q8", &bn_act_fwd_q8), py::arg("y"), py::arg("scale"),
         py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"));
   m.def("conv_fwd_fp8", checked("conv_fwd_fp8", &conv_fwd_fp8), py::arg("x"), py::arg("wq"), py::arg("oscale"),
-        py::arg("stride"), py::arg("pad"), py::arg("stats"));
+        py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("ascale") = py::none());
+  m.def("conv_dgrad_fp8", checked("conv_dgrad_fp8", &conv_dgrad_fp8), py::arg("dy8"), py::arg("wt8"),
+        py::arg("wscale"), py::arg("ascale"), py::arg("x_shape"), py::arg("stride"), py::arg("pad"),
+        py::arg("addend") = py::none());
+  m.def("conv_dgrad_bn_fp8", checked("conv_dgrad_bn_fp8", &conv_dgrad_bn_fp8), py::arg("dy8"), py::arg("wt8"),
+        py::arg("wscale"), py::arg("ascale"), py::arg("x_shape"), py::arg("stride"), py::arg("pad"),
+        py::arg("addend"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
+        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+  m.def("bn_act_bwd_apply_q8", checked("bn_act_bwd_apply_q8", &bn_act_bwd_apply_q8));
+  m.def("quant_rows_e4m3", checked("quant_rows_e4m3", &quant_rows_e4m3));
+  m.def("quant_rows_entry_bytes", []() { return (int64_t)pdt::quant_rows_entry_bytes(); });
   m.def("mfma_f8_probe", checked("mfma_f8_probe", &mfma_f8_probe), py::arg("a"), py::arg("b"),
         py::arg("fmt_a") = 0, py::arg("fmt_b") = 0, py::arg("scale_a") = 127, py::arg("scale_b") = 127,
         py::arg("use_scale") = true);

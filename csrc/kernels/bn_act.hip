@@ -7,6 +7,7 @@
 // merge) + ONE read-y/write-z pass.  Backward is one reduction pass over
 // (dz, z, y) and one elementwise pass producing dy and the residual gradient.
 #include "common.h"
+#include "fp8_util.h"
 #include "kernels.h"
 
 #include <cstdlib>
@@ -422,13 +423,20 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
 // ------------------------------------------------------------- backward apply
 // Grid-stride with gridDim*256 a multiple of K/8, so every thread keeps one fixed 8-channel
 // group: the per-channel coefficients are computed once per thread, not per element.
-template <int MASK, bool TRAIN, bool DRES>
+// Q8: also dy8 = e5m2(bf16(dy) * s_t) with delayed scaling (fp8_util.h) for an fp8 dgrad
+template <int MASK, bool TRAIN, bool DRES, bool Q8 = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const uint4* __restrict__ dz, const uint4* __restrict__ z, const uint4* __restrict__ y,
     const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ sums, int64_t nvec, int K8, float invM, uint4* __restrict__ dy,
-    uint4* __restrict__ dres) {
+    uint4* __restrict__ dres, uint2* __restrict__ dy8 = nullptr, float* __restrict__ state = nullptr,
+    int slot = 0) {
   const int K = K8 * 8;
+  float qs = 1.f, qm = 0.f;
+  if constexpr (Q8) {
+    qs = delayed_scale<true>(state, slot);
+    publish_scale(state, slot, qs);
+  }
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(tid % K8) * 8;
@@ -461,9 +469,21 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       gr.v[j] = g;
       o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
     }
-    dy[v] = pack8(o);
+    const uint4 ob = pack8(o);
+    dy[v] = ob;
     if (DRES) dres[v] = pack8(gr);
+    if constexpr (Q8) {
+      const f8 r = unpack8(ob);  // quantize exactly the bf16 dy the weight gradient reads
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qm = fmaxf(qm, fabsf(r.v[j]));
+        t[j] = r.v[j] * qs;
+      }
+      dy8[v] = make_uint2(cvt4_e5m2(t[0], t[1], t[2], t[3]), cvt4_e5m2(t[4], t[5], t[6], t[7]));
+    }
   }
+  if constexpr (Q8) block_amax(qm, state + slot * SLOT_FLOATS);
 }
 
 void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
@@ -490,6 +510,31 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   else { PDT_BWD_T(0) }
 #undef PDT_BWD_T
 #undef PDT_BWD
+}
+
+void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
+                                const float* stats, const float* gamma, const float* sums, int mask,
+                                bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
+                                uint8_t* dy8, float* state, int slot, hipStream_t st) {
+  if (!training) throw std::runtime_error("bn_act_bwd_apply_q8: training mode only");
+  int64_t nvec = M * K / 8;
+  int K8 = K / 8;
+  int64_t b = (nvec + 255) / 256;
+  dim3 g((unsigned)(b < 4096 ? b : 4096)), blk(256);  // multiple of K8: 256 % K8 == 0 (checked by binding)
+  auto DZ = reinterpret_cast<const uint4*>(dz);
+  auto Z = reinterpret_cast<const uint4*>(z);
+  auto Y = reinterpret_cast<const uint4*>(y);
+  auto DY = reinterpret_cast<uint4*>(dy);
+  auto DR = reinterpret_cast<uint4*>(dres);
+  auto D8 = reinterpret_cast<uint2*>(dy8);
+  float invM = 1.f / (float)M;
+#define PDT_BWDQ(MK, DRS)                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, true, DRS, true>), g, blk, 0, st, DZ, Z, Y, stats, \
+                     gamma, sums, nvec, K8, invM, DY, DR, D8, state, slot)
+  if (mask == 1) { if (dres) PDT_BWDQ(1, true); else PDT_BWDQ(1, false); }
+  else if (mask == 2) { if (dres) PDT_BWDQ(2, true); else PDT_BWDQ(2, false); }
+  else { if (dres) PDT_BWDQ(0, true); else PDT_BWDQ(0, false); }
+#undef PDT_BWDQ
 }
 
 void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float* sums,

@@ -106,6 +106,7 @@ struct NtArgs {
   const uint16_t* addend;  // optional NHWC tensor (same layout as out) added in the epilogue
   float* part;         // BN partials [ngroups][2][Nout] or null
   const float* oscale; // fp8 operands: per-output-column dequantization factor (acc * oscale[col])
+  const float* ascale; // fp8 operands: activation dequantization factor (device scalar) or null
   uint32_t a_bytes, b_bytes;
   int HA, WA, CA;      // A source dims
   int Nout, Kg, S;     // GEMM N, B row length (= taps_total*CA), filter width (generic path)
@@ -365,11 +366,13 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 
   if constexpr (OP != OP_BF16) {
     // fp8: back to real units with the per-column factor (weight scale x activation scale)
+    const float as = P.ascale != nullptr ? P.ascale[0] : 1.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = wcol0 + j * 16 + fq * 4;
-      const float4 sc = col < P.Nout ? *reinterpret_cast<const float4*>(P.oscale + col)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 sc = col < P.Nout ? *reinterpret_cast<const float4*>(P.oscale + col)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      sc.x *= as; sc.y *= as; sc.z *= as; sc.w *= as;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         acc[i][j][0] *= sc.x; acc[i][j][1] *= sc.y; acc[i][j][2] *= sc.z; acc[i][j][3] *= sc.w;
@@ -901,12 +904,12 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   }
 }
 
-void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, uint16_t* y,
-                         float* part, const ConvShape& s, hipStream_t st) {
+void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, const float* ascale,
+                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st) {
   if (s.C % 16 != 0) throw std::runtime_error("conv_fwd_fp8: input channels must be a multiple of 16");
   NtArgs a{};
   a.a = reinterpret_cast<const uint16_t*>(x); a.b = reinterpret_cast<const uint16_t*>(w);
-  a.out = y; a.part = part; a.oscale = oscale;
+  a.out = y; a.part = part; a.oscale = oscale; a.ascale = ascale;
   a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C);
   a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C);
   a.HA = s.H; a.WA = s.W; a.CA = s.C;
@@ -946,17 +949,22 @@ int conv_dgrad_bn_groups(const ConvShape& s) {
   return g;
 }
 
-void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn) {
-  if (s.K % 64 != 0) throw std::runtime_error("conv_dgrad: output channels must be a multiple of 64");
+template <int OP>
+static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale, const float* ascale,
+                            uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
+                            const BnBwdFuse* bn) {
+  constexpr int EB = OP == OP_BF16 ? 2 : 1;
+  if (s.K % (128 / EB) != 0)
+    throw std::runtime_error("conv_dgrad: output channels must fill 128-byte rows (64 bf16 / 128 fp8)");
   const int str = s.stride;
   int group0 = 0;
   for (int ph = 0; ph < str; ++ph)
     for (int pw = 0; pw < str; ++pw) {
       NtArgs a{};
-      a.a = dy; a.b = wt; a.out = dx; a.addend = addend; a.part = nullptr;
-      a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
-      a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * 2);
+      a.a = reinterpret_cast<const uint16_t*>(dy); a.b = reinterpret_cast<const uint16_t*>(wt);
+      a.out = dx; a.addend = addend; a.part = nullptr; a.oscale = oscale; a.ascale = ascale;
+      a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * EB);
+      a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * EB);
       a.HA = s.Ho; a.WA = s.Wo; a.CA = s.K;
       a.Nout = s.C; a.Kg = s.R * s.S * s.K; a.S = s.S;
       const int Mi = (s.H - ph + str - 1) / str;
@@ -979,11 +987,22 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
         a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part;
         a.bn_mask = bn->mask; a.bn_group0 = group0;
         group0 += ceil_div(a.M, conv_fwd_group_rows(a.M, a.Nout));
-        dispatch_nt<true, EPI_BNB>(a, st, nullptr);
+        dispatch_nt<true, EPI_BNB, OP>(a, st, nullptr);
       } else {
-        dispatch_nt<true, EPI_PLAIN>(a, st, nullptr);
+        dispatch_nt<true, EPI_PLAIN, OP>(a, st, nullptr);
       }
     }
+}
+
+void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn) {
+  conv_dgrad_impl<OP_BF16>(dy, wt, nullptr, nullptr, dx, addend, s, st, bn);
+}
+
+void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,
+                           uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
+                           const BnBwdFuse* bn) {
+  conv_dgrad_impl<OP_F8_E5M2>(dy, wt, oscale, ascale, dx, addend, s, st, bn);
 }
 
 // ------------------------------------------------------------------- wgrad

@@ -10,11 +10,15 @@
 // verified by tests/test_fp8_gpu.py against exact integer data), fp8 weight packing with
 // per-output-channel scales, and delayed-scaling activation quantization.
 #include "common.h"
+#include "fp8_util.h"
 #include "kernels.h"
 
 #include <stdexcept>
 
 namespace pdt {
+
+int fp8_state_floats() { return DEQ_OFFSET + 4; }
+int fp8_deq_offset() { return DEQ_OFFSET; }
 
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 
@@ -43,54 +47,6 @@ void launch_mfma_f8_probe(const void* a_regs, const void* b_regs, float* d, int 
     hipLaunchKernelGGL((mfma_f8_probe_kernel<0, 1>), dim3(1), dim3(64), 0, st, A, B, D, scale_a, scale_b, use_scale);
   else
     hipLaunchKernelGGL((mfma_f8_probe_kernel<1, 1>), dim3(1), dim3(64), 0, st, A, B, D, scale_a, scale_b, use_scale);
-}
-
-// ------------------------------------------------------------------ conversion
-constexpr float E4M3_MAX = 448.f;
-constexpr float E5M2_MAX = 57344.f;
-
-// two floats -> two e4m3 bytes (low 16 bits), saturating (the hardware convert does not clamp)
-__device__ __forceinline__ uint32_t cvt2_e4m3(float a, float b) {
-  a = fminf(fmaxf(a, -E4M3_MAX), E4M3_MAX);
-  b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
-  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
-}
-__device__ __forceinline__ uint32_t cvt4_e4m3(float a, float b, float c, float d) {
-  return cvt2_e4m3(a, b) | (cvt2_e4m3(c, d) << 16);
-}
-
-// Delayed per-tensor scaling (state = float[6]: amax of the last three calls, then the three
-// dequantization factors).  Call t quantizes with s_t = 2^floor(log2(E4M3_HEADROOM / amax_{t-1}))
-// (1 before any history), publishes deq[t%3] = 1/s_t for its consumers, accumulates amax_t into
-// slot t%3 and clears slot (t+1)%3 for the next call -- no host sync, no extra launch.
-constexpr float E4M3_HEADROOM = 224.f;  // one binade of margin below 448 for growth between steps
-
-__device__ __forceinline__ float delayed_scale(const float* state, int slot) {
-  const float prev = state[(slot + 2) % 3];
-  if (!(prev > 0.f)) return 1.f;
-  const float s = exp2f(floorf(log2f(E4M3_HEADROOM / prev)));
-  return fminf(fmaxf(s, 1.f / 1048576.f), 1048576.f);
-}
-
-__device__ __forceinline__ void publish_scale(float* state, int slot, float s) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    state[3 + slot] = 1.f / s;
-    state[(slot + 1) % 3] = 0.f;
-  }
-}
-
-// block max of a non-negative value, one atomic per block (float bits order as uint for x >= 0)
-__device__ __forceinline__ void block_amax(float v, float* dst) {
-  __shared__ float sm[16];
-  v = wave_max(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sm[w] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float m = sm[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, sm[i]);
-    atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(m));
-  }
 }
 
 // ------------------------------------------------------------------ weights
@@ -144,6 +100,48 @@ void launch_pack_weight_fp8(const float* w, const int64_t* strides, uint8_t* wq,
                      S, Cp);
 }
 
+// Row-wise e4m3 quantization of bf16 weight images living in one flat mirror (KRSC rows = one
+// output channel each for the forward, CRSK rows = one input channel for dgrad): one wave per
+// row, scale[row] = amax(row)/448, q = e4m3(w / scale).  One launch for every conv of the model.
+struct QRowEntry { int64_t off, soff; int rows, rowlen; };
+
+__global__ void __launch_bounds__(256) quant_rows_e4m3_kernel(const uint16_t* __restrict__ src,
+                                                              uint8_t* __restrict__ dst,
+                                                              float* __restrict__ scale,
+                                                              const QRowEntry* __restrict__ tab) {
+  const QRowEntry e = tab[blockIdx.y];
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= e.rows) return;
+  const int lane = threadIdx.x & 63;
+  const uint4* r = reinterpret_cast<const uint4*>(src + e.off + (int64_t)row * e.rowlen);
+  const int nv = e.rowlen / 8;
+  float m = 0.f;
+  for (int v = lane; v < nv; v += 64) {
+    const f8 a = unpack8(r[v]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(a.v[j]));
+  }
+  m = wave_max(m);
+  const float sc = m > 0.f ? m / E4M3_MAX : 1.f;
+  if (lane == 0) scale[e.soff + row] = sc;
+  const float inv = 1.f / sc;
+  uint2* o = reinterpret_cast<uint2*>(dst + e.off + (int64_t)row * e.rowlen);
+  for (int v = lane; v < nv; v += 64) {
+    const f8 a = unpack8(r[v]);
+    o[v] = make_uint2(cvt4_e4m3(a.v[0] * inv, a.v[1] * inv, a.v[2] * inv, a.v[3] * inv),
+                      cvt4_e4m3(a.v[4] * inv, a.v[5] * inv, a.v[6] * inv, a.v[7] * inv));
+  }
+}
+
+void launch_quant_rows_e4m3(const uint16_t* src, uint8_t* dst, float* scale, const void* table,
+                            int ntensors, int max_rows, hipStream_t st) {
+  if (ntensors <= 0) return;
+  hipLaunchKernelGGL(quant_rows_e4m3_kernel, dim3((max_rows + 3) / 4, ntensors), dim3(256), 0, st, src, dst,
+                     scale, reinterpret_cast<const QRowEntry*>(table));
+}
+
+size_t quant_rows_entry_bytes() { return sizeof(QRowEntry); }
+
 // ------------------------------------------------------------------ activations
 // bf16 -> e4m3 with delayed scaling (8 elements = one 16-B load, one 8-B store per thread-step)
 __global__ void __launch_bounds__(256) quant_e4m3_kernel(const uint4* __restrict__ x, uint2* __restrict__ q,
@@ -162,7 +160,7 @@ __global__ void __launch_bounds__(256) quant_e4m3_kernel(const uint4* __restrict
     }
     q[v] = make_uint2(cvt4_e4m3(t[0], t[1], t[2], t[3]), cvt4_e4m3(t[4], t[5], t[6], t[7]));
   }
-  block_amax(m, state + slot);
+  block_amax(m, state + slot * SLOT_FLOATS);
 }
 
 static int q_blocks(int64_t nvec) {
@@ -221,7 +219,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd_q8_kernel(const uint4* __restr
     }
     q[v] = make_uint2(cvt4_e4m3(t[0], t[1], t[2], t[3]), cvt4_e4m3(t[4], t[5], t[6], t[7]));
   }
-  block_amax(m, state + slot);
+  block_amax(m, state + slot * SLOT_FLOATS);
 }
 
 void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* shift, const uint16_t* res,

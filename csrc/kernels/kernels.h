@@ -147,15 +147,35 @@ struct WStridesF8 { int64_t k, c, r, s; };
 // epilogue's dequantization factor for column k.
 void launch_pack_weight_fp8(const float* w, const int64_t* strides, uint8_t* wq, float* oscale,
                             const float* act_deq, int K, int C, int R, int S, int Cp, hipStream_t st);
-// Delayed-scaling state: float[6] = amax of the last 3 calls, then their dequant factors;
-// `slot` = call index % 3 (kept by the caller).  deq of this call lands in state[3 + slot].
+// Delayed-scaling state: float[fp8_state_floats()] = sharded amax of the last 3 calls, then their
+// dequant factors; `slot` = call index % 3 (kept by the caller).  The dequant factor of this call
+// lands in state[fp8_deq_offset() + slot].
+int fp8_state_floats();
+int fp8_deq_offset();
 void launch_quant_e4m3(const uint16_t* x, uint8_t* q, int64_t n, float* state, int slot, hipStream_t st);
 // bn_act_fwd that also writes the e4m3 copy q of z (same delayed-scaling contract)
 void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* shift, const uint16_t* res,
                           bool relu, uint16_t* z, uint8_t* q, int64_t M, int K, float* state, int slot,
                           hipStream_t st);
-// fp8 forward conv: x e4m3 NHWC (C % 16 == 0), w e4m3 [K][R][S][C], y bf16 = (x*w) * oscale[k]
-void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, uint16_t* y,
-                         float* part, const ConvShape& s, hipStream_t st);
+// Batched row-wise e4m3 quantization of bf16 weight images in a flat mirror: table = device
+// array of ntensors {int64 off (elements, same in src and dst), int64 soff (first scale index),
+// int rows, int rowlen (multiple of 8)}; scale[soff + row] = amax(row) / 448.
+void launch_quant_rows_e4m3(const uint16_t* src, uint8_t* dst, float* scale, const void* table,
+                            int ntensors, int max_rows, hipStream_t st);
+size_t quant_rows_entry_bytes();
+// fp8 forward conv: x e4m3 NHWC (C % 16 == 0), w e4m3 [K][R][S][C],
+// y bf16 = (x*w) * oscale[k] * (ascale ? ascale[0] : 1)
+void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, const float* ascale,
+                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st);
+// fp8 dgrad: dy e5m2 NHWC (K % 128 == 0), wt e4m3 [C][R][S][K] with per-C scale oscale[c],
+// activation (dy) dequant factor ascale[0]; otherwise as launch_conv_dgrad
+void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,
+                           uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
+                           const BnBwdFuse* bn = nullptr);
+// bn_act_bwd_apply that also writes dy8 = e5m2(bf16(dy) * s_t) (delayed scaling, fp8 state contract)
+void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
+                                const float* stats, const float* gamma, const float* sums, int mask,
+                                bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
+                                uint8_t* dy8, float* state, int slot, hipStream_t st);
 
 }  // namespace pdt

@@ -33,6 +33,7 @@ _FUSE_DGRAD_BN = os.environ.get("PDT_DGRAD_BN", "1") != "0"
 _BN_HANDOFF = os.environ.get("PDT_BN_HANDOFF", "1") != "0"
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
 _FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
+_FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input-gradient GEMMs
 
 
 def set_fp8(on: bool) -> None:
@@ -50,10 +51,12 @@ def fp8_enabled() -> bool:
 class _Q8State:
     """Delayed-scaling state of one fp8 activation producer (csrc/kernels/fp8.hip contract)."""
 
-    __slots__ = ("buf", "t")
+    __slots__ = ("buf", "t", "off")
 
     def __init__(self, device):
-        self.buf = torch.zeros(6, dtype=torch.float32, device=device)
+        C = native()
+        self.buf = torch.zeros(C.fp8_state_floats(), dtype=torch.float32, device=device)
+        self.off = C.fp8_deq_offset()
         self.t = 0
 
     def next_slot(self) -> int:
@@ -62,15 +65,49 @@ class _Q8State:
         return slot
 
     def deq(self, slot: int) -> torch.Tensor:
-        return self.buf.narrow(0, 3 + slot, 1)
+        return self.buf.narrow(0, self.off + slot, 1)
 
 
-def _q8_state(owner: nn.Module, device) -> _Q8State:
-    st = getattr(owner, "_pdt_q8", None)
+def _q8_state(owner, device, attr: str = "_pdt_q8") -> _Q8State:
+    """Delayed-scaling state kept on ``owner`` (a module for forward activations, the BN gamma
+    Parameter for backward gradients)."""
+    st = getattr(owner, attr, None)
     if st is None or st.buf.device != device:
         st = _Q8State(device)
-        owner._pdt_q8 = st
+        setattr(owner, attr, st)
     return st
+
+
+def _rows_e4m3(C, src2d: torch.Tensor):
+    """Row-wise e4m3 quantization of one bf16 [rows, n] image (fallback when no flat mirror)."""
+    import numpy as np
+    rows, n = src2d.shape
+    dt = np.dtype([("off", "<i8"), ("soff", "<i8"), ("rows", "<i4"), ("rowlen", "<i4")])
+    tab = torch.from_numpy(np.array([(0, 0, rows, n)], dtype=dt).view(np.uint8).copy()).to(src2d.device)
+    q = torch.empty(src2d.numel(), dtype=torch.uint8, device=src2d.device)
+    sc = torch.empty(rows, dtype=torch.float32, device=src2d.device)
+    C.quant_rows_e4m3(src2d.reshape(-1), q, sc, tab, rows)
+    return q, sc
+
+
+def _packed_krsc8(C, w, cx):
+    """(e4m3 [K,R,S,Cx], per-K scale) forward weights: flat-mirror view or a fresh pack."""
+    m = _mirror_of(w)
+    v = m.krsc8_view(w) if m is not None and w.shape[1] == cx else None
+    if v is not None:
+        return v
+    return C.pack_weight_fp8(w, cx)
+
+
+def _packed_crsk8(C, w):
+    """(e4m3 [C,R,S,K], per-C scale) dgrad weights: flat-mirror view or a fresh pack."""
+    m = _mirror_of(w)
+    v = m.crsk8_view(w) if m is not None else None
+    if v is not None:
+        return v
+    k, c, r, s = w.shape
+    q, sc = _rows_e4m3(C, C.pack_weight_t(w).view(c, r * s * k))
+    return q.view(c, r, s, k), sc
 
 
 def fp8_attach(x: torch.Tensor, owner: nn.Module) -> torch.Tensor:
@@ -409,8 +446,8 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     n, h, wd, cx = x.shape
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
     if x8 is not None:
-        wq, osc = C.pack_weight_fp8(w, cx, x8[1])
-        y, part = C.conv_fwd_fp8(x8[0], wq, osc, stride, pad, training)
+        wq, wsc = _packed_krsc8(C, w, cx)
+        y, part = C.conv_fwd_fp8(x8[0], wq, wsc, stride, pad, training, x8[1])
     else:
         wk = _packed_krsc(C, w, cx)
         y, part = C.conv_fwd(x, wk, stride, pad, training)
@@ -494,6 +531,7 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.spec = spec
         ctx.ntensors = len(tensors)
         ctx.handoff_in = handoff  # the producer of x (previous block), or None
+        ctx.fp8b = fp8io is not None and _FP8_BWD  # fp8 dgrads in backward (dy in e5m2)
         _, y_last, st_last = outs[-1]
         ctx.handoff_out = _BnHandoff(y_last, st_last, tensors[5 * (nch - 1) + 1],
                                      tensors[5 * (nch - 1) + 2])
@@ -551,16 +589,41 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j + 2] = sums_[0]
             return sums_
 
-        def dgrad_bn(j, dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_):
+        def apply(j, dz_, z_, y_, stt_, sums_, mask_, tr_, want_dres, need_dgrad):
+            """BN backward apply of unit j -> (dy, dres, d8); d8 = (e5m2 dy, its dequant factor)
+            when the dgrad consuming dy runs on fp8"""
+            gamma_ = tensors[j + 1]
+            if ctx.fp8b and tr_ and need_dgrad and dz_.shape[3] % 128 == 0:
+                stq = _q8_state(params[j + 1], dz_.device, "_pdt_q8b")
+                slot = stq.next_slot()
+                dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_, y_, stt_, gamma_, sums_, mask_, want_dres,
+                                                       stq.buf, slot)
+                return dy_, dres_, (q_, stq.deq(slot))
+            dy_, dres_ = C.bn_act_bwd_apply(dz_, z_, y_, stt_, gamma_, sums_, mask_, tr_, want_dres)
+            return dy_, dres_, None
+
+        def dgrad(dy_, d8_, w_, xshape, st_, pd_, addend_):
+            if d8_ is not None:
+                wt8, wsc = _packed_crsk8(C, w_)
+                return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
+            return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
+
+        def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None):
+            if d8_ is not None:
+                wt8, wsc = _packed_crsk8(C, w_)
+                return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
+                                           stt_, mask_, sg, sb)
+            return C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb,
+                                   _packed_crsk(w_))
+
+        def dgrad_bn(j, dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_):
             """input gradient of a conv + BN backward reduction of unit j (its producer)"""
             sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
             if sg is not None and sb is not None:
-                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_,
-                                            sg, sb, _packed_crsk(w_))
+                g_, sums_ = dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb)
                 sunk.extend([params[j + 1], params[j + 2]])
             else:
-                g_, sums_ = C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_,
-                                            wt=_packed_crsk(w_))
+                g_, sums_ = dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_)
                 grads[j + 1] = sums_[1] * stt_[1]
                 grads[j + 2] = sums_[0]
             return g_, sums_
@@ -588,13 +651,14 @@ class _ResidualBlock(torch.autograd.Function):
             w, gamma = tensors[5 * i], tensors[5 * i + 1]
             xin = x if i == 0 else units[i - 1][0]
             last = i == nch - 1
+            need_dx = i > 0 or ctx.needs_input_grad[0]
             if pre is None:
                 mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
                 sums = bnreduce(5 * i, dz, z, y, stt, mask)
-                dy, dres = C.bn_act_bwd_apply(dz, z, y, stt, gamma, sums, mask, tr, last)
+                dy, dres, d8 = apply(5 * i, dz, z, y, stt, sums, mask, tr, last, need_dx)
             else:
                 g, sums = pre  # g = dz * relu'(unit i), reduced in the producing epilogue
-                dy, _ = C.bn_act_bwd_apply(g, g, y, stt, gamma, sums, 0, tr, False)
+                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx)
                 dres = g
             pre = None
             wgrad(5 * i, dy, xin, st, pd)
@@ -603,19 +667,19 @@ class _ResidualBlock(torch.autograd.Function):
             if i > 0:
                 yp, sttp = units[i - 1][1], units[i - 1][2]
                 if _FUSE_DGRAD_BN:
-                    pre = dgrad_bn(5 * (i - 1), dy, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
+                    pre = dgrad_bn(5 * (i - 1), dy, d8, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
                 else:
-                    dz = C.conv_dgrad(dy, w, list(xin.shape), st, pd, wt=_packed_crsk(w))
+                    dz = dgrad(dy, d8, w, list(xin.shape), st, pd, None)
             else:
                 # shortcut gradient: identity -> g_short itself; projection -> its dgrad
                 if ds_cfg is not None:
                     st2, pd2, tr2, _, _ = ds_cfg
-                    wds, gds = tensors[5 * nch], tensors[5 * nch + 1]
+                    wds = tensors[5 * nch]
                     sums_ds = bnreduce(5 * nch, g_short, g_short, y_ds, st_ds, 0)
-                    dy_ds, _ = C.bn_act_bwd_apply(g_short, g_short, y_ds, st_ds, gds, sums_ds,
-                                                  0, tr2, False)
+                    dy_ds, _, d8_ds = apply(5 * nch, g_short, g_short, y_ds, st_ds, sums_ds, 0, tr2, False,
+                                            ctx.needs_input_grad[0])
                     wgrad(5 * nch, dy_ds, x, st2, pd2)
-                    addend = C.conv_dgrad(dy_ds, wds, list(x.shape), st2, pd2, wt=_packed_crsk(wds))
+                    addend = dgrad(dy_ds, d8_ds, wds, list(x.shape), st2, pd2, None)
                 else:
                     addend = g_short
                 if not ctx.needs_input_grad[0]:
@@ -626,11 +690,11 @@ class _ResidualBlock(torch.autograd.Function):
                     sb = _grad_sink(hi.beta) if hi is not None else None
                     if sg is not None and sb is not None and _BN_HANDOFF and _FUSE_DGRAD_BN:
                         # previous block's last unit: relu mask from its output z = x
-                        dz, sums_in = C.conv_dgrad_bn(dy, w, list(x.shape), st, pd, addend, hi.y, x,
-                                                      hi.stats, 1, sg, sb, _packed_crsk(w))
+                        dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, x,
+                                                   hi.stats, 1, sg, sb)
                         hi.deposit = (dz, sums_in)
                     else:
-                        dz = C.conv_dgrad(dy, w, list(x.shape), st, pd, addend, _packed_crsk(w))
+                        dz = dgrad(dy, d8, w, list(x.shape), st, pd, addend)
         ctx.handoff_in = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)

@@ -158,6 +158,71 @@ class WeightMirror:
         self.ntensors = len(ent)
         self.max_tiles = max((e[3] * e[4] * e[5] for e in ent), default=0)
         self.key = None
+        self._ent = ent
+        self._fp8 = None  # e4m3 images of both layouts with per-row scales, built on first use
+        self.key8 = None
+
+    # ---------------------------------------------------------------- fp8 (e4m3) images
+    def _build_fp8(self) -> None:
+        import numpy as np
+        from ..ops._ext import native
+        C = native()
+        dev = self.krsc.device
+        dt = np.dtype([("off", "<i8"), ("soff", "<i8"), ("rows", "<i4"), ("rowlen", "<i4")])
+        assert dt.itemsize == C.quant_rows_entry_bytes(), "QRowEntry layout mismatch"
+        tk, tc = [], []
+        ks = cs = 0
+        self._kscale_at, self._cscale_at = {}, {}
+        for p, (o, k, c, rs, _, _, _) in zip(self._tracked, self._ent):
+            tk.append((o, ks, k, rs * c))
+            tc.append((o, cs, c, rs * k))
+            self._kscale_at[id(p)] = (ks, k)
+            self._cscale_at[id(p)] = (cs, c)
+            ks += k
+            cs += c
+        mk = lambda t: torch.from_numpy(np.array(t, dtype=dt).view(np.uint8).copy()).to(dev)  # noqa: E731
+        self._fp8 = {
+            "krsc8": torch.empty(self.space.numel, dtype=torch.uint8, device=dev),
+            "crsk8": torch.empty(self.space.numel, dtype=torch.uint8, device=dev),
+            "kscale": torch.empty(max(ks, 1), dtype=torch.float32, device=dev),
+            "cscale": torch.empty(max(cs, 1), dtype=torch.float32, device=dev),
+            "tk": mk(tk), "tc": mk(tc),
+            "mk": max((e[2] for e in tk), default=0), "mc": max((e[2] for e in tc), default=0),
+        }
+
+    def ensure_fp8(self) -> bool:
+        """Quantize both bf16 images to e4m3 (one launch each) if they changed since last time."""
+        if not self.valid() or not self._tracked:
+            return False
+        if self._fp8 is None:
+            self._build_fp8()
+        if self.key8 != self.key:
+            from ..ops._ext import native
+            C, f = native(), self._fp8
+            C.quant_rows_e4m3(self.krsc, f["krsc8"], f["kscale"], f["tk"], f["mk"])
+            C.quant_rows_e4m3(self.crsk, f["crsk8"], f["cscale"], f["tc"], f["mc"])
+            self.key8 = self.key
+        return True
+
+    def krsc8_view(self, p):
+        """(e4m3 [K,R,S,C], per-K scale [K]) of a tracked conv weight, or None."""
+        if id(p) not in self._krsc_views or not self.ensure_fp8():
+            return None
+        k, c, r, s_ = p.shape
+        o = self._krsc_views[id(p)].storage_offset() - self.krsc.storage_offset()
+        a, n = self._kscale_at[id(p)]
+        return (self._fp8["krsc8"].narrow(0, o, p.numel()).view(k, r, s_, c),
+                self._fp8["kscale"].narrow(0, a, n))
+
+    def crsk8_view(self, p):
+        """(e4m3 [C,R,S,K], per-C scale [C]) of a tracked conv weight, or None."""
+        if id(p) not in self._crsk_views or not self.ensure_fp8():
+            return None
+        k, c, r, s_ = p.shape
+        o = self._crsk_views[id(p)].storage_offset() - self.crsk.storage_offset()
+        a, n = self._cscale_at[id(p)]
+        return (self._fp8["crsk8"].narrow(0, o, p.numel()).view(c, r, s_, k),
+                self._fp8["cscale"].narrow(0, a, n))
 
     def current_key(self):
         # a Parameter re-homed with ``p.data = view`` keeps its own version counter

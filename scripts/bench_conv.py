@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--torch", action="store_true", help="also time MIOpen via torch")
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="single shape CxHxWxKxRxSxstridexpad")
+    ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3) forward conv")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda:0")
@@ -73,7 +74,9 @@ def main():
     rows = []
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "t_fwd": 0.0, "t_dgrad": 0.0, "t_wgrad": 0.0, "flop": 0.0}
     print("C,H,W,K,R,S,st,pd,count,M,N,K_gemm,fwd_ms,fwd_TF,dgrad_ms,dgrad_TF,wgrad_ms,wgrad_TF"
-          + (",torch_fwd_ms,torch_dgrad_ms,torch_wgrad_ms" if a.torch else ""))
+          + (",torch_fwd_ms,torch_dgrad_ms,torch_wgrad_ms" if a.torch else "")
+          + (",fp8_fwd_ms,fp8_fwd_TF" if a.fp8 else ""))
+    tot["f8_fwd"] = 0.0
     shapes = conv_shapes(a.arch, N, a.image)
     if a.only:
         want = tuple(int(v) for v in a.only.split("x"))
@@ -110,6 +113,17 @@ def main():
             tot["t_fwd"] += tf * cnt
             tot["t_dgrad"] += td * cnt
             tot["t_wgrad"] += tw * cnt
+        if a.fp8:
+            if cx % 16 == 0:
+                st8 = torch.zeros(C.fp8_state_floats(), device=dev)
+                x8 = C.quant_e4m3(x, st8, 0)
+                d0 = C.fp8_deq_offset()
+                wq, osc = C.pack_weight_fp8(wt, cx, st8[d0:d0 + 1])
+                f8 = timeit(lambda: C.conv_fwd_fp8(x8, wq, osc, st, pd, True), a.iters)
+            else:
+                f8 = f
+            row += [round(f8, 3), round(flop / f8 / 1e9, 1)]
+            tot["f8_fwd"] += f8 * cnt
         print(",".join(str(v) for v in row), flush=True)
         rows.append(row)
     summ = {k: round(v, 3) for k, v in tot.items() if k != "flop"}
