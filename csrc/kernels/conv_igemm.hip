@@ -108,6 +108,7 @@ struct NtArgs {
   const float* oscale; // fp8 operands: per-output-column dequantization factor (acc * oscale[col])
   const float* ascale; // fp8 operands: activation dequantization factor (device scalar) or null
   uint32_t a_bytes, b_bytes;
+  uint32_t o_bytes;    // bytes of the output tensor (= of addend / bn_y / bn_z, same layout)
   int HA, WA, CA;      // A source dims
   int Nout, Kg, S;     // GEMM N, B row length (= taps_total*CA), filter width (generic path)
   int M;               // GEMM rows of this launch
@@ -454,10 +455,25 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       bsq[q] = 0.f;
     }
   }
-  for (int qd = lane; qd < CHUNKS; qd += 64) {
-    int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-    int m = wrow0 + r;
-    int col = wcol0 + c * 8;
+  // Two phases per batch of up to 8 chunks: first issue every global read the epilogue needs
+  // (BN y / z, residual-gradient addend) -- bounds-checked buffer loads, OOB lanes read 0 --
+  // then combine and store.  One exposed memory latency per batch instead of one per chunk (the
+  // compiler cannot hoist a load above a store that may alias it); batches bound the registers.
+  constexpr int IT_ALL = CHUNKS / 64;
+  constexpr int IT_MAX = 4;  // 4 x (y, z, addend) chunks in flight: occupancy stays as without batching
+  constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
+  static_assert(IT_ALL % IT == 0, "chunk batches");
+  const bool has_add = P.addend != nullptr;
+#pragma unroll 1
+  for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
+  uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int qd = lane + (b0 + it) * 64;
+    const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+    const int m = wrow0 + r;
+    const int col = wcol0 + c * 8;
+    ooff[it] = OOB;
     if (m < P.M && col < P.Nout) {
       int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
       if (!P.dense) {    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
@@ -467,34 +483,59 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
         uint32_t jj = rem - ii * (uint32_t)P.Mj;
         orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
       }
-      v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
-      if (P.addend != nullptr) {  // fused residual-gradient sum (block input of a residual block)
-        f8 a = unpack8(__builtin_bit_cast(uint4, v));
-        f8 b = unpack8(*reinterpret_cast<const uint4*>(P.addend + orow * P.Nout + col));
-#pragma unroll
-        for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
-        v = __builtin_bit_cast(v4i, pack8(a));
-      }
-      if constexpr (EPI == EPI_BNB) {
-        // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
-        // partial sums agree bit for bit with what the apply pass reads back
-        f8 a = unpack8(__builtin_bit_cast(uint4, v));
-        const f8 yv = unpack8(*reinterpret_cast<const uint4*>(P.bn_y + orow * P.Nout + col));
-        f8 zv;
-        if (P.bn_mask == 1) zv = unpack8(*reinterpret_cast<const uint4*>(P.bn_z + orow * P.Nout + col));
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const bool on = P.bn_mask == 1 ? zv.v[q] > 0.f
-                        : (P.bn_mask == 2 ? fmaf(yv.v[q], bsc[q], bsh[q]) > 0.f : true);
-          const float g = on ? a.v[q] : 0.f;
-          a.v[q] = g;
-          bsg[q] += g;
-          bsq[q] = fmaf(g, yv.v[q] - bmu[q], bsq[q]);
-        }
-        v = __builtin_bit_cast(v4i, pack8(a));
-      }
-      *reinterpret_cast<v4i*>(P.out + orow * P.Nout + col) = v;
+      ooff[it] = (uint32_t)((orow * P.Nout + col) * 2);
     }
+  }
+  v4i av[IT], yv[IT], zv[IT];
+  if (has_add) {
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.o_bytes);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, ooff[it]);
+  }
+  if constexpr (EPI == EPI_BNB) {
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
+    if (P.bn_mask == 1) {
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int qd = lane + (b0 + it) * 64;
+    const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+    v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+    if (has_add) {  // fused residual-gradient sum (block input of a residual block)
+      f8 a = unpack8(__builtin_bit_cast(uint4, v));
+      const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
+      v = __builtin_bit_cast(v4i, pack8(a));
+    }
+    if constexpr (EPI == EPI_BNB) {
+      // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
+      // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
+      // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
+      f8 a = unpack8(__builtin_bit_cast(uint4, v));
+      const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
+      f8 zz;
+      if (P.bn_mask == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
+      const bool valid = ooff[it] != OOB;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const bool on = valid && (P.bn_mask == 1 ? zz.v[q] > 0.f
+                                  : (P.bn_mask == 2 ? fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f : true));
+        const float g = on ? a.v[q] : 0.f;
+        a.v[q] = g;
+        bsg[q] += g;
+        bsq[q] = fmaf(g, yy.v[q] - bmu[q], bsq[q]);
+      }
+      v = __builtin_bit_cast(v4i, pack8(a));
+    }
+    if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
+  }
   }
   if constexpr (EPI == EPI_BNB) {
     // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
@@ -884,6 +925,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.a = x; a.b = w; a.out = y; a.part = part;
   a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
   a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C * 2);
+  a.o_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
   a.HA = s.H; a.WA = s.W; a.CA = s.C;
   a.Nout = s.K; a.Kg = s.R * s.S * s.C; a.S = s.S;
   a.M = s.N * s.Ho * s.Wo;
@@ -912,6 +954,7 @@ void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale
   a.out = y; a.part = part; a.oscale = oscale; a.ascale = ascale;
   a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C);
   a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C);
+  a.o_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
   a.HA = s.H; a.WA = s.W; a.CA = s.C;
   a.Nout = s.K; a.Kg = s.R * s.S * s.C; a.S = s.S;
   a.M = s.N * s.Ho * s.Wo;
@@ -965,6 +1008,7 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       a.out = dx; a.addend = addend; a.part = nullptr; a.oscale = oscale; a.ascale = ascale;
       a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * EB);
       a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * EB);
+      a.o_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
       a.HA = s.Ho; a.WA = s.Wo; a.CA = s.K;
       a.Nout = s.C; a.Kg = s.R * s.S * s.K; a.S = s.S;
       const int Mi = (s.H - ph + str - 1) / str;

@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="single shape CxHxWxKxRxSxstridexpad")
     ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3) forward conv")
+    ap.add_argument("--bn", action="store_true", help="also time dgrad with the fused BN-backward epilogue")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda:0")
@@ -75,7 +76,9 @@ def main():
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "t_fwd": 0.0, "t_dgrad": 0.0, "t_wgrad": 0.0, "flop": 0.0}
     print("C,H,W,K,R,S,st,pd,count,M,N,K_gemm,fwd_ms,fwd_TF,dgrad_ms,dgrad_TF,wgrad_ms,wgrad_TF"
           + (",torch_fwd_ms,torch_dgrad_ms,torch_wgrad_ms" if a.torch else "")
-          + (",fp8_fwd_ms,fp8_fwd_TF" if a.fp8 else ""))
+          + (",fp8_fwd_ms,fp8_fwd_TF" if a.fp8 else "")
+          + (",dgrad_bn_ms" if a.bn else ""))
+    tot["dgrad_bn"] = 0.0
     tot["f8_fwd"] = 0.0
     shapes = conv_shapes(a.arch, N, a.image)
     if a.only:
@@ -124,6 +127,17 @@ def main():
                 f8 = f
             row += [round(f8, 3), round(flop / f8 / 1e9, 1)]
             tot["f8_fwd"] += f8 * cnt
+        if a.bn:
+            if c % 8 == 0:
+                yb = torch.randn(N, h, w, c, device=dev).to(torch.bfloat16)
+                stt = torch.stack([torch.zeros(c, device=dev), torch.ones(c, device=dev),
+                                   torch.ones(c, device=dev), torch.zeros(c, device=dev)])
+                db = timeit(lambda: C.conv_dgrad_bn(dy, wt, [N, h, w, c], st, pd, None, yb, None, stt, 2),
+                            a.iters)
+            else:
+                db = 0.0
+            row += [round(db, 3)]
+            tot["dgrad_bn"] += db * cnt
         print(",".join(str(v) for v in row), flush=True)
         rows.append(row)
     summ = {k: round(v, 3) for k, v in tot.items() if k != "flop"}
