@@ -604,28 +604,43 @@ __device__ __forceinline__ int swz128_tr(int row, int chunk) {
   return row * 128 + ((chunk ^ (sw << 1)) << 4);
 }
 
+// 512-B rows (the [64 m][256 kout] dy tile of a BMG = 256 wgrad): the swz256 XOR on chunk bits
+// 1..3 -- LDS banks repeat every 256 B, so a half-wave's rows {m..m+3, m+8..m+11} still land in 8
+// distinct 32-B bank windows.
+__device__ __forceinline__ int swz512(int row, int chunk) {
+  int sw = (row & 3) | (((row >> 3) & 1) << 2);
+  return row * 512 + ((chunk ^ (sw << 1)) << 4);
+}
+
 template <int ROWB>
 __device__ __forceinline__ int swz_img(int row, int chunk) {
-  if constexpr (ROWB == 256) return swz256(row, chunk);
+  if constexpr (ROWB == 512) return swz512(row, chunk);
+  else if constexpr (ROWB == 256) return swz256(row, chunk);
   else return swz128_tr(row, chunk);
 }
 
 template <int BMG, int BNG, int STAGES>
 struct TnCfg {
-  static_assert(BNG == 128 && (BMG == 64 || BMG == 128), "TN tile shapes");
+  static_assert(BNG == 128 && (BMG == 64 || BMG == 128 || BMG == 256), "TN tile shapes");
   static_assert(STAGES >= 2 && STAGES <= 3, "pipeline depth");
-  static constexpr int NT = 256;
+  // waves: 2 x 2 (64x64 or 32x64 per wave) up to BMG = 128; 4 x 2 of 64x64 for BMG = 256, which
+  // halves the B (activation gather) loads and their per-row address math per MFMA
+  static constexpr int WAVES_M = BMG == 256 ? 4 : 2;
+  static constexpr int WAVES_N = 2;
+  static constexpr int WAVES = WAVES_M * WAVES_N;
+  static constexpr int NT = 64 * WAVES;
   static constexpr int A_ROWB = BMG * 2;              // bytes per m row of the dy tile image
   static constexpr int A_BYTES = 64 * A_ROWB;
   static constexpr int B_BYTES = 64 * 256;            // [64 m][128 col], 256-B rows
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int SMEM = STAGES * STAGE;
-  static constexpr int TM = BMG / 2 / 16;             // 2x2 waves
-  static constexpr int TN = BNG / 2 / 16;
+  static constexpr int TM = BMG / WAVES_M / 16;
+  static constexpr int TN = BNG / WAVES_N / 16;
   static constexpr int A_LPR = A_ROWB / 16;           // lanes per row in one 1-KiB DMA instruction
   static constexpr int A_RPI = 64 / A_LPR;            // rows per instruction
-  static constexpr int A_PW = A_BYTES / 1024 / 4;     // DMA instructions per wave per tile
-  static constexpr int B_PW = B_BYTES / 1024 / 4;
+  static constexpr int A_PW = A_BYTES / 1024 / WAVES;  // DMA instructions per wave per tile
+  static constexpr int B_PW = B_BYTES / 1024 / WAVES;
+  static_assert(A_PW * 1024 * WAVES == A_BYTES && B_PW * 1024 * WAVES == B_BYTES, "tile DMA split");
 };
 
 // Main loop as igemm_nt (LDS-DMA, source-side swizzle, 2 buffers, one barrier per K-step).  One
@@ -634,9 +649,13 @@ struct TnCfg {
 // Grid: 1-D over (split, tile) with split-major logical ids after the XCD remap, so the
 // column tiles of one split -- which read the same dy rows and overlapping x rows -- run on
 // the same XCD and share its L2.
+template <int BMG>
+constexpr int tn_threads() { return BMG == 256 ? 512 : 256; }  // == TnCfg<BMG, ...>::NT
+
 template <int BMG, int BNG, int STAGES, bool ATOMIC>
-__global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
+__global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
   using CFG = TnCfg<BMG, BNG, STAGES>;
+  static_assert(CFG::NT == tn_threads<BMG>(), "launch bounds");
   constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -710,7 +729,7 @@ __global__ void __launch_bounds__(256) igemm_tn_kernel(const TnArgs P) {
     }
   };
 
-  const int wm = wid & 1, wn = wid >> 1;
+  const int wm = wid % CFG::WAVES_M, wn = wid / CFG::WAVES_M;
   const int li = lane & 15, g = lane >> 4;  // group g covers k rows 8g..8g+7
   // tr-read address pieces: lane 4q+p of a group -> row q, columns 4p..4p+3
   const int tq = li >> 2, tp = li & 3;
@@ -1069,13 +1088,21 @@ struct WgradPlan {
 
 static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   WgradPlan p;
-  p.bmg = s.K <= 64 ? 64 : 128;
+  // PDT_TN_WIDE=1: 8-wave 256x128 tile when Kout % 256 == 0.  It halves the activation-gather
+  // loads and their address math per MFMA, but measured 5-20% SLOWER on every ResNet-50 wgrad
+  // shape (one 96-KB block per CU hides less latency than two 4-wave 48-KB blocks), so it is off.
+  static int wide = -1;
+  if (wide < 0) {
+    const char* e = getenv("PDT_TN_WIDE");
+    wide = (e && e[0] == '1') ? 1 : 0;
+  }
+  p.bmg = s.K <= 64 ? 64 : ((wide && s.K % 256 == 0) ? 256 : 128);
   p.bng = 128;
   const int ncols = s.R * s.S * s.C;
   p.tiles = ((s.K + p.bmg - 1) / p.bmg) * ((ncols + p.bng - 1) / p.bng);
   const int64_t mred = (int64_t)s.N * s.Ho * s.Wo;
   p.nsteps = (int)((mred + 63) / 64);
-  int target = 1024;  // ~4 blocks per CU
+  int target = p.bmg == 256 ? 512 : 1024;  // ~4 4-wave (2 8-wave) blocks per CU
   int splits = (target + p.tiles - 1) / p.tiles;
   splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
   // bound the reduction traffic: atomics/slabs move splits * |dW| * 4 bytes
@@ -1104,7 +1131,7 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(tiles * splits), dim3(256), CFG::SMEM, st, a);
+  hipLaunchKernelGGL(kfn, dim3(tiles * splits), dim3(CFG::NT), CFG::SMEM, st, a);
   check_launch("igemm_tn");
 }
 
@@ -1130,7 +1157,10 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
-  if (p.bmg == 64) {
+  if (p.bmg == 256) {
+    if (atomic) run_tn<256, 128, 2, true>(a, p.tiles, p.splits, st);
+    else run_tn<256, 128, 2, false>(a, p.tiles, p.splits, st);
+  } else if (p.bmg == 64) {
     if (deep) { if (atomic) run_tn<64, 128, 3, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 3, false>(a, p.tiles, p.splits, st); }
     else { if (atomic) run_tn<64, 128, 2, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false>(a, p.tiles, p.splits, st); }
   } else {
