@@ -564,6 +564,35 @@ void quant_rows_e4m3(const Tensor& src, Tensor dst, Tensor scale, const Tensor& 
                               (int)(table.numel() / eb), (int)max_rows, cur_stream(src));
 }
 
+// ---------------------------------------------------------------- augment
+// images: uint8 or fp32 [N,C,H,W] (device); idx/oy/ox int64 [B]; flip bool [B] or None
+Tensor augment(const Tensor& images, const Tensor& idx, const Tensor& oy, const Tensor& ox,
+               const std::optional<Tensor>& flip, int64_t pad, bool normalize, std::vector<double> mean,
+               std::vector<double> stdv) {
+  check_cuda(images, "images");
+  TORCH_CHECK(images.dim() == 4 && (images.scalar_type() == at::kByte || images.scalar_type() == at::kFloat),
+              "images must be uint8 or fp32 NCHW");
+  for (const Tensor* t : {&idx, &oy, &ox})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == idx.numel(),
+                "idx/oy/ox must be device int64 [B]");
+  const bool* fp = nullptr;
+  if (flip.has_value() && flip->defined()) {
+    TORCH_CHECK(flip->is_cuda() && flip->scalar_type() == at::kBool && flip->numel() == idx.numel(),
+                "flip must be device bool [B]");
+    fp = flip->data_ptr<bool>();
+  }
+  TORCH_CHECK(mean.size() >= (size_t)images.size(1) && stdv.size() >= (size_t)images.size(1), "mean/std per channel");
+  c10::hip::HIPGuard g(images.get_device());
+  const int B = idx.numel(), C = images.size(1), H = images.size(2), W = images.size(3);
+  float m[3] = {0.f, 0.f, 0.f}, sd[3] = {1.f, 1.f, 1.f};
+  for (int c = 0; c < C; ++c) { m[c] = (float)mean[c]; sd[c] = (float)stdv[c]; }
+  auto out = at::empty({B, C, H, W}, images.options().dtype(at::kFloat));
+  pdt::launch_augment(images.data_ptr(), images.scalar_type() == at::kByte, idx.data_ptr<int64_t>(),
+                      oy.data_ptr<int64_t>(), ox.data_ptr<int64_t>(), fp, out.data_ptr<float>(), B, C, H, W,
+                      (int)pad, normalize, m, sd, cur_stream(images));
+  return out;
+}
+
 // -------------------------------------------------------------------- pool
 std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x) {
   check_bf16_nhwc(x, "x");
@@ -813,6 +842,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_bwd_reduce", checked("bn_act_bwd_reduce", &bn_act_bwd_reduce), py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply));
+  m.def("augment", checked("augment", &augment), py::arg("images"), py::arg("idx"), py::arg("oy"), py::arg("ox"),
+        py::arg("flip"), py::arg("pad"), py::arg("normalize"), py::arg("mean"), py::arg("std"));
   m.def("maxpool_fwd", checked("maxpool_fwd", &maxpool_fwd));
   m.def("maxpool_bwd", checked("maxpool_bwd", &maxpool_bwd));
   m.def("avgpool_fwd", checked("avgpool_fwd", &avgpool_fwd));

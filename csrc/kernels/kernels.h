@@ -135,6 +135,14 @@ void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float
 void launch_cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t st);
 void launch_cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t st);
 
+// ------------------------------------------------------------- augment.hip
+// Fused gather + RandomCrop(pad) + RandomHorizontalFlip + (/255) + Normalize of a device-resident
+// NCHW dataset (uint8 or fp32) into fp32 NCHW out[B][C][H][W]; per-sample crop offsets oy/ox in
+// [0, 2*pad] and flip flags (may be null) are drawn by the caller.  mean/std: host arrays of 3.
+void launch_augment(const void* src, bool src_u8, const int64_t* idx, const int64_t* oy, const int64_t* ox,
+                    const bool* flip, float* out, int B, int C, int H, int W, int pad, bool normalize,
+                    const float* mean, const float* stdv, hipStream_t st);
+
 // ----------------------------------------------------------------- fp8.hip
 // One v_mfma_scale_f32_16x16x128_f8f6f4 on raw per-lane operand registers (64 lanes x 32 bytes
 // each for A and B), D = 64 lanes x 4 fp32.  fmt 0 = e4m3, 1 = e5m2; scales are E8M0 bytes

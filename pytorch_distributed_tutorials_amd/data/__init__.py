@@ -6,5 +6,5 @@ from .datasets import (  # noqa: F401
     cifar10,
     synthetic_dataset,
 )
-from .loader import DeviceLoader, random_crop_flip  # noqa: F401
+from .loader import DeviceLoader, draw_crop_flip, random_crop_flip  # noqa: F401
 from .sampler import DistributedSampler  # noqa: F401

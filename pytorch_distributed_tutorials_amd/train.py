@@ -79,9 +79,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-steps-per-epoch", type=int, default=None)
     p.add_argument("--timeout", type=float, default=None, help="collective timeout (s)")
     p.add_argument("--log-every", type=int, default=0, help="print img/s every N steps (0 = off)")
-    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
-                   help="compute dtype: native kernels are bf16 (fp32 master weights); the torch "
-                        "path runs fp32 (reference) or bf16 autocast; auto = bf16 native / fp32 torch")
+    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32", "fp8"],
+                   help="compute dtype: native kernels are bf16 (fp32 master weights), or fp8 convs "
+                        "(e4m3 forward / e5m2 input gradients, delayed scaling); the torch path runs "
+                        "fp32 (reference) or bf16 autocast; auto = bf16 native / fp32 torch")
     p.add_argument("--steps", type=int, default=None, help="stop after this many training steps in total")
     p.add_argument("--trace", action="store_true",
                    help="emit roctx ranges (fwd/bwd/step/eval) for rocprofv3 --marker-trace")
@@ -120,8 +121,12 @@ def main(argv: Optional[list] = None) -> int:
     dtype = args.dtype
     if dtype == "auto":
         dtype = "bf16" if impl == "native" else "fp32"
-    if impl == "native" and dtype != "bf16":
-        raise SystemExit("--impl native computes in bf16 (fp32 master weights); use --impl torch for fp32")
+    if impl == "native" and dtype not in ("bf16", "fp8"):
+        raise SystemExit("--impl native computes in bf16 or fp8 (fp32 master weights); use --impl torch for fp32")
+    if dtype == "fp8":
+        if impl != "native" or device.type != "cuda":
+            raise SystemExit("--dtype fp8 needs the native impl on a GPU")
+        ops.set_fp8(True)
     autocast = (impl == "torch" and dtype == "bf16")
     if args.trace:
         trace.enable(True)

@@ -534,3 +534,24 @@ def test_wgrad_into_sink_ignores_uninitialised_workspace(gpu, native_ext, determ
     finally:
         torch.use_deterministic_algorithms(old_det)
         torch.utils.deterministic.fill_uninitialized_memory = old_fill
+
+
+@pytest.mark.parametrize("normalized", [False, True])
+@pytest.mark.parametrize("augment", [True, False])
+def test_fused_augment_matches_torch_loader(gpu, native_ext, normalized, augment):
+    """The fused HIP gather/crop/flip/normalize kernel == the batched torch loader, bit for bit."""
+    from pytorch_distributed_tutorials_amd.data import DeviceLoader, TensorImageDataset
+    g = torch.Generator().manual_seed(21)
+    if normalized:
+        imgs = torch.randn(40, 3, 32, 32, generator=g)
+    else:
+        imgs = torch.randint(0, 256, (40, 3, 32, 32), generator=g, dtype=torch.uint8)
+    ds = TensorImageDataset(imgs, torch.randint(0, 10, (40,), generator=g), normalized=normalized)
+    kw = dict(batch_size=16, shuffle=True, augment=augment, device=gpu, seed=3)
+    fused = list(DeviceLoader(ds, fused=True, **kw))
+    plain = list(DeviceLoader(ds, fused=False, **kw))
+    assert len(fused) == len(plain) == 3
+    for (xa, ya), (xb, yb) in zip(fused, plain):
+        assert torch.equal(ya, yb)
+        assert xa.dtype == torch.float32 and xa.shape == xb.shape
+        assert torch.equal(xa, xb)
