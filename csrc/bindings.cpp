@@ -205,13 +205,18 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
               "dgrad_bn: y must have the shape of x");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * s.C && stats.is_contiguous(),
               "stats must be fp32 [4, C]");
-  TORCH_CHECK(mask >= 0 && mask <= 2, "mask must be 0, 1 or 2");
+  TORCH_CHECK(mask >= 0 && mask <= 3, "mask must be 0, 1, 2 or 3");
   const uint16_t* zp = nullptr;
   if (mask == 1) {
     TORCH_CHECK(z.has_value() && z->defined(), "mask 1 needs z");
     check_bf16_nhwc(*z, "z");
     TORCH_CHECK(z->sizes() == y.sizes(), "z shape mismatch");
     zp = cbf(*z);
+  } else if (mask == 3) {  // ReLU bitmask from bn_act_fwd_mask: one byte per 8 channels
+    TORCH_CHECK(z.has_value() && z->defined(), "mask 3 needs the ReLU bitmask");
+    check_cuda(*z, "zmask");
+    TORCH_CHECK(z->scalar_type() == at::kByte && z->numel() * 8 == y.numel(), "zmask must be uint8 [numel/8]");
+    zp = reinterpret_cast<const uint16_t*>(z->data_ptr());
   }
   auto dx = at::empty({s.N, s.H, s.W, s.C}, y.options());
   const uint16_t* ap = nullptr;
@@ -471,6 +476,27 @@ Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
   pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z), M,
                          K, cur_stream(y));
   return z;
+}
+
+// (z, zmask): bn_act_fwd with ReLU that also writes the 1-bit-per-element ReLU mask (uint8, one
+// byte per 8 channels) for a later BN-fused dgrad (mask mode 3)
+std::tuple<Tensor, Tensor> bn_act_fwd_mask(const Tensor& y, const Tensor& scale, const Tensor& shift,
+                                           const std::optional<Tensor>& res) {
+  check_bf16_nhwc(y, "y");
+  c10::hip::HIPGuard g(y.get_device());
+  int K = y.size(3);
+  int64_t M = y.numel() / K;
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_nhwc(*res, "residual");
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
+    rp = cbf(*res);
+  }
+  auto z = at::empty_like(y);
+  auto zm = at::empty({y.numel() / 8}, y.options().dtype(at::kByte));
+  pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, true, bf(z), M, K,
+                         cur_stream(y), zm.data_ptr<uint8_t>());
+  return {z, zm};
 }
 
 Tensor bn_act_bwd_reduce(const Tensor& dz, const Tensor& z, const Tensor& y, const Tensor& stats,
@@ -745,9 +771,10 @@ Tensor quant_e4m3(const Tensor& x, Tensor state, int64_t slot) {
   return q;
 }
 
-std::tuple<Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, const Tensor& shift,
-                                         const std::optional<Tensor>& res, bool relu, Tensor state,
-                                         int64_t slot) {
+// (z, q, zmask); zmask is undefined unless want_mask (needs relu)
+std::tuple<Tensor, Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, const Tensor& shift,
+                                                 const std::optional<Tensor>& res, bool relu, Tensor state,
+                                                 int64_t slot, bool want_mask) {
   check_bf16_nhwc(y, "y");
   check_state(state, slot);
   c10::hip::HIPGuard g(y.get_device());
@@ -759,11 +786,15 @@ std::tuple<Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, c
     TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
     rp = cbf(*res);
   }
+  TORCH_CHECK(!want_mask || relu, "a ReLU mask needs relu");
   auto z = at::empty_like(y);
   auto q = at::empty(y.sizes(), y.options().dtype(at::kByte));
+  Tensor zm;
+  if (want_mask) zm = at::empty({y.numel() / 8}, y.options().dtype(at::kByte));
   pdt::launch_bn_act_fwd_q8(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z),
-                            q.data_ptr<uint8_t>(), M, K, state.data_ptr<float>(), (int)slot, cur_stream(y));
-  return {z, q};
+                            q.data_ptr<uint8_t>(), M, K, state.data_ptr<float>(), (int)slot, cur_stream(y),
+                            want_mask ? zm.data_ptr<uint8_t>() : nullptr);
+  return {z, q, zm};
 }
 
 std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const Tensor& oscale,
@@ -839,6 +870,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"));
+  m.def("bn_act_fwd_mask", checked("bn_act_fwd_mask", &bn_act_fwd_mask), py::arg("y"), py::arg("scale"),
+        py::arg("shift"), py::arg("residual"));
   m.def("bn_act_bwd_reduce", checked("bn_act_bwd_reduce", &bn_act_bwd_reduce), py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply));
@@ -862,7 +895,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fp8_state_floats", &pdt::fp8_state_floats);
   m.def("fp8_deq_offset", &pdt::fp8_deq_offset);
   m.def("bn_act_fwd_q8", checked("bn_act_fwd_q8", &bn_act_fwd_q8), py::arg("y"), py::arg("scale"),
-        py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"));
+        py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"),
+        py::arg("want_mask") = false);
   m.def("conv_fwd_fp8", checked("conv_fwd_fp8", &conv_fwd_fp8), py::arg("x"), py::arg("wq"), py::arg("oscale"),
         py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("ascale") = py::none());
   m.def("conv_dgrad_fp8", checked("conv_dgrad_fp8", &conv_dgrad_fp8), py::arg("dy8"), py::arg("wt8"),

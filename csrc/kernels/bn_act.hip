@@ -175,13 +175,13 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 }
 
 // ------------------------------------------------------------------- forward
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool MASK = false>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const uint4* __restrict__ res,
                                                          uint4* __restrict__ z, int64_t nvec,
-                                                         int K8) {
+                                                         int K8, uint8_t* __restrict__ zmask = nullptr) {
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     int c0 = (int)(v % K8) * 8;
@@ -201,7 +201,15 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
       if (RELU) t = fmaxf(t, 0.f);
       a.v[j] = t;
     }
-    z[v] = pack8(a);
+    const uint4 zb = pack8(a);
+    z[v] = zb;
+    if constexpr (MASK) {  // bit j = stored bf16 z > 0 (exactly what a z read would test)
+      const f8 zr = unpack8(zb);
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (zr.v[j] > 0.f ? 1u : 0u) << j;
+      zmask[v] = (uint8_t)bits;
+    }
   }
 }
 
@@ -212,14 +220,18 @@ static int ew_blocks(int64_t nvec) {
 
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
-                       hipStream_t st) {
+                       hipStream_t st, uint8_t* zmask) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
   dim3 g(ew_blocks(nvec)), b(256);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto R = reinterpret_cast<const uint4*>(res);
   auto Z = reinterpret_cast<uint4*>(z);
-  if (res) {
+  if (zmask) {
+    if (!relu) throw std::runtime_error("bn_act_fwd: a ReLU mask needs relu");
+    if (res) hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8, zmask);
+    else hipLaunchKernelGGL((bn_act_fwd_kernel<false, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8, zmask);
+  } else if (res) {
     if (relu) hipLaunchKernelGGL((bn_act_fwd_kernel<true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
     else hipLaunchKernelGGL((bn_act_fwd_kernel<true, false>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
   } else {

@@ -113,6 +113,7 @@ struct NtArgs {
   int Nout, Kg, S;     // GEMM N, B row length (= taps_total*CA), filter width (generic path)
   int M;               // GEMM rows of this launch
   FastDiv div_ij, div_j;  // m -> n = m / Mij, i = rem / Mj
+  FastDiv div_ca, div_s;  // generic (non-C64) loader: k -> tap = k / CA, tap -> r = tap / S
   int Mij, Mj;
   int ash, asw, aoff_h, aoff_w;     // A base coords: h0 = i*ash + aoff_h
   int OH, OW, osh, osw, oph, opw;   // out row = (n*OH + i*osh + oph)*OW + j*osw + opw
@@ -125,7 +126,8 @@ struct NtArgs {
   // epilogue.  out = g = dx * relu'(unit) and per-(wave rows, channel) partials of
   // (sum g, sum g*(y - mean)) go to bn_part[bn_group0 + wave_row_group][2][Nout].
   const uint16_t* bn_y;   // that unit's pre-BN conv output (same layout as out)
-  const uint16_t* bn_z;   // its post-activation output (mask mode 1 only)
+  const uint16_t* bn_z;   // its post-activation output (mask mode 1 only), or for mask mode 3 its
+                          // ReLU bitmask: one byte per 8-channel chunk, bit q = (z[c0 + q] > 0)
   const float* bn_stats;  // [4][Nout] mean, invstd, scale, shift
   float* bn_part;
   int bn_mask, bn_group0;
@@ -278,9 +280,9 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
         const int kk = kt * KE + a_c[i] * CE;
-        const int tap = kk / P.CA;
+        const int tap = (int)fdiv((uint32_t)kk, P.div_ca);  // mul-hi, not a runtime divide
         const int ch = kk - tap * P.CA;
-        const int r = tap / P.S;
+        const int r = (int)fdiv((uint32_t)tap, P.div_s);
         const int s = tap - r * P.S;
         int h = a_h0[i] + r, w = a_w0[i] + s;
         bool ok = kk < P.Kg && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
@@ -500,6 +502,11 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
 #pragma unroll
       for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
+    } else if (P.bn_mask == 3) {  // 1 byte per 16-B chunk instead of the 16-B z chunk
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes >> 4);
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        zv[it][0] = (int)__builtin_amdgcn_raw_buffer_load_b8(rz, ooff[it] == OOB ? OOB : ooff[it] >> 4, 0, 0);
     }
   }
 #pragma unroll
@@ -522,10 +529,12 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
       f8 zz;
       if (P.bn_mask == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
+      const uint32_t zbits = P.bn_mask == 3 ? (uint32_t)zv[it][0] : 0u;
       const bool valid = ooff[it] != OOB;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const bool on = valid && (P.bn_mask == 1 ? zz.v[q] > 0.f
+                                  : P.bn_mask == 3 ? ((zbits >> q) & 1u) != 0u
                                   : (P.bn_mask == 2 ? fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f : true));
         const float g = on ? a.v[q] : 0.f;
         a.v[q] = g;
@@ -936,6 +945,8 @@ static void fill_common(NtArgs& a, int Mi, int Mj) {
   a.Mj = Mj;
   a.div_ij = make_fastdiv((uint32_t)a.Mij);
   a.div_j = make_fastdiv((uint32_t)Mj);
+  a.div_ca = make_fastdiv((uint32_t)a.CA);
+  a.div_s = make_fastdiv((uint32_t)a.S);
 }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,

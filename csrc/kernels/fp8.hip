@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd_q8_kernel(const uint4* __restr
                                                             const uint4* __restrict__ res,
                                                             uint4* __restrict__ z, uint2* __restrict__ q,
                                                             int64_t nvec, int K8, float* __restrict__ state,
-                                                            int slot) {
+                                                            int slot, uint8_t* __restrict__ zmask) {
   const float s = delayed_scale(state, slot);
   publish_scale(state, slot, s);
   float m = 0.f;
@@ -212,11 +212,14 @@ __global__ void __launch_bounds__(256) bn_act_fwd_q8_kernel(const uint4* __restr
     z[v] = zb;
     const f8 zr = unpack8(zb);  // quantize exactly the bf16 value the bf16 consumers see
     float t[8];
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       m = fmaxf(m, fabsf(zr.v[j]));
       t[j] = zr.v[j] * s;
+      bits |= (zr.v[j] > 0.f ? 1u : 0u) << j;
     }
+    if (zmask != nullptr) zmask[v] = (uint8_t)bits;
     q[v] = make_uint2(cvt4_e4m3(t[0], t[1], t[2], t[3]), cvt4_e4m3(t[4], t[5], t[6], t[7]));
   }
   block_amax(m, state + slot * SLOT_FLOATS);
@@ -224,7 +227,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd_q8_kernel(const uint4* __restr
 
 void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* shift, const uint16_t* res,
                           bool relu, uint16_t* z, uint8_t* q, int64_t M, int K, float* state, int slot,
-                          hipStream_t st) {
+                          hipStream_t st, uint8_t* zmask) {
   const int64_t nvec = M * K / 8;
   const int K8 = K / 8;
   dim3 g(q_blocks(nvec)), b(256);
@@ -233,11 +236,11 @@ void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* sh
   auto Z = reinterpret_cast<uint4*>(z);
   auto Q = reinterpret_cast<uint2*>(q);
   if (res) {
-    if (relu) hipLaunchKernelGGL((bn_act_fwd_q8_kernel<true, true>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot);
-    else hipLaunchKernelGGL((bn_act_fwd_q8_kernel<true, false>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot);
+    if (relu) hipLaunchKernelGGL((bn_act_fwd_q8_kernel<true, true>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot, zmask);
+    else hipLaunchKernelGGL((bn_act_fwd_q8_kernel<true, false>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot, zmask);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_act_fwd_q8_kernel<false, true>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot);
-    else hipLaunchKernelGGL((bn_act_fwd_q8_kernel<false, false>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot);
+    if (relu) hipLaunchKernelGGL((bn_act_fwd_q8_kernel<false, true>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot, zmask);
+    else hipLaunchKernelGGL((bn_act_fwd_q8_kernel<false, false>), g, b, 0, st, Y, scale, shift, R, Z, Q, nvec, K8, state, slot, zmask);
   }
 }
 

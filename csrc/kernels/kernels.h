@@ -60,7 +60,8 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
 // launch_bn_bwd_part_reduce.
 struct BnBwdFuse {
   const uint16_t* y;     // [N,H,W,C] pre-BN output of that unit
-  const uint16_t* z;     // [N,H,W,C] its activation output (mask 1) or null
+  const uint16_t* z;     // [N,H,W,C] its activation output (mask 1), its ReLU bitmask (mask 3:
+                         // uint8 [N*H*W*C/8], bit q of byte i = z[8i + q] > 0), or null
   const float* stats;    // [4][C] mean, invstd, scale, shift
   float* part;           // [G][2][C]
   int mask;
@@ -86,10 +87,11 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
                         float* out, hipStream_t st);
 void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma, const float* beta,
                            float eps, int K, float* out, hipStream_t st);
-// z = act(y*scale + shift (+res))
+// z = act(y*scale + shift (+res)); zmask (optional, with relu): one byte per 8 channels, bit q =
+// z[8i + q] > 0 -- the ReLU mask a later backward reads instead of z (1/16 of the bytes)
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
-                       hipStream_t st);
+                       hipStream_t st, uint8_t* zmask = nullptr);
 // Backward BN.  stats = bn_finalize output [4][K] (mean, invstd, scale, shift).  mask: 0 = no
 // ReLU, 1 = ReLU mask from z (> 0), 2 = ReLU mask recomputed from y (y*scale + shift > 0).
 // sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * mask; ws >= bn_bwd_ws_floats(M, K)
@@ -164,7 +166,7 @@ void launch_quant_e4m3(const uint16_t* x, uint8_t* q, int64_t n, float* state, i
 // bn_act_fwd that also writes the e4m3 copy q of z (same delayed-scaling contract)
 void launch_bn_act_fwd_q8(const uint16_t* y, const float* scale, const float* shift, const uint16_t* res,
                           bool relu, uint16_t* z, uint8_t* q, int64_t M, int K, float* state, int slot,
-                          hipStream_t st);
+                          hipStream_t st, uint8_t* zmask = nullptr);
 // Batched row-wise e4m3 quantization of bf16 weight images in a flat mirror: table = device
 // array of ntensors {int64 off (elements, same in src and dst), int64 soff (first scale index),
 // int rows, int rowlen (multiple of 8)}; scale[soff + row] = amax(row) / 448.

@@ -31,6 +31,7 @@ _CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
 # and its cross-block handoff
 _FUSE_DGRAD_BN = os.environ.get("PDT_DGRAD_BN", "1") != "0"
 _BN_HANDOFF = os.environ.get("PDT_BN_HANDOFF", "1") != "0"
+_ZMASK = os.environ.get("PDT_ZMASK", "1") != "0"  # 1-bit ReLU masks for the handoff (else read z)
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
 _FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
 _FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input-gradient GEMMs
@@ -439,12 +440,15 @@ def _packed_crsk(w):
 
 
 def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual,
-              x8=None, q8=None):
-    """conv -> BN -> (+residual) -> (ReLU).  x8 = (e4m3 copy of x, its dequant factor): fp8 conv;
-    q8 = _Q8State: also emit the e4m3 copy of the output (returned as the 4th value)."""
+              x8=None, q8=None, want_mask=False):
+    """conv -> BN -> (+residual) -> (ReLU) -> (z, y, stats, z8, zmask).  x8 = (e4m3 copy of x, its
+    dequant factor): fp8 conv; q8 = _Q8State: also emit the e4m3 copy z8 of the output;
+    want_mask (with relu): also the 1-bit ReLU mask zmask a later BN-fused dgrad reads instead of z."""
     k, _, r, s = w.shape
     n, h, wd, cx = x.shape
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
+    if x8 is not None and r * s * cx < 256:
+        x8 = None  # a GEMM K of 64 (1x1 over 64 channels) half-fills the 128-wide fp8 K-step: bf16 is faster
     if x8 is not None:
         wq, wsc = _packed_krsc8(C, w, cx)
         y, part = C.conv_fwd_fp8(x8[0], wq, wsc, stride, pad, training, x8[1])
@@ -459,12 +463,16 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:
         stats = C.bn_eval_params(rm, rv, gamma, beta, float(eps))
+    want_mask = want_mask and relu
     if q8 is not None and k % 16 == 0:
         slot = q8.next_slot()
-        z, zq = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot)
-        return z, y, stats, (zq, q8.deq(slot))
+        z, zq, zm = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot, want_mask)
+        return z, y, stats, (zq, q8.deq(slot)), (zm if want_mask else None)
+    if want_mask:
+        z, zm = C.bn_act_fwd_mask(y, stats[2], stats[3], residual)
+        return z, y, stats, None, zm
     z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu)
-    return z, y, stats, None
+    return z, y, stats, None, None
 
 
 class _BnHandoff:
@@ -473,10 +481,10 @@ class _BnHandoff:
     dgrad epilogue.  The consumer deposits (g, sums); the producer uses them only if the
     gradient it receives IS that g (same storage: no other consumer added to it)."""
 
-    __slots__ = ("y", "stats", "gamma", "beta", "deposit")
+    __slots__ = ("y", "stats", "gamma", "beta", "zmask", "deposit")
 
-    def __init__(self, y, stats, gamma, beta):
-        self.y, self.stats, self.gamma, self.beta = y, stats, gamma, beta
+    def __init__(self, y, stats, gamma, beta, zmask=None):
+        self.y, self.stats, self.gamma, self.beta, self.zmask = y, stats, gamma, beta, zmask
         self.deposit = None
 
 
@@ -507,16 +515,22 @@ class _ResidualBlock(torch.autograd.Function):
         if ds_cfg is not None:
             w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
             st, pd, tr, mo, ep = ds_cfg
-            res, y_ds, st_ds, _ = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None, x8)
+            res, y_ds, st_ds, _, _ = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None, x8)
         else:
             res = x
         h, h8 = x, x8
         outs = []
+        zmask = None
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
             last = i == nch - 1
-            z, y, stt, h8 = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
-                                      res if last else None, h8, q8s[i] if q8s else None)
+            # the block output's ReLU mask as bits: the next block's BN-fused dgrad reads it
+            # instead of z (1/16 of the bytes)
+            z, y, stt, h8, zm = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
+                                          res if last else None, h8, q8s[i] if q8s else None,
+                                          want_mask=last and tr and _ZMASK and _BN_HANDOFF and _FUSE_DGRAD_BN)
+            if last:
+                zmask = zm
             outs.append((z, y, stt))
             h = z
         if holder is not None and h8 is not None:
@@ -534,7 +548,7 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.fp8b = fp8io is not None and _FP8_BWD  # fp8 dgrads in backward (dy in e5m2)
         _, y_last, st_last = outs[-1]
         ctx.handoff_out = _BnHandoff(y_last, st_last, tensors[5 * (nch - 1) + 1],
-                                     tensors[5 * (nch - 1) + 2])
+                                     tensors[5 * (nch - 1) + 2], zmask)
         return h
 
     @staticmethod
@@ -690,8 +704,9 @@ class _ResidualBlock(torch.autograd.Function):
                     sb = _grad_sink(hi.beta) if hi is not None else None
                     if sg is not None and sb is not None and _BN_HANDOFF and _FUSE_DGRAD_BN:
                         # previous block's last unit: relu mask from its output z = x
-                        dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, x,
-                                                   hi.stats, 1, sg, sb)
+                        zsrc, zmode = (hi.zmask, 3) if hi.zmask is not None else (x, 1)
+                        dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
+                                                   hi.stats, zmode, sg, sb)
                         hi.deposit = (dz, sums_in)
                     else:
                         dz = dgrad(dy, d8, w, list(x.shape), st, pd, addend)

@@ -183,9 +183,11 @@ def test_bn_act_fwd_q8_matches_bf16_apply(gpu, native_ext):
     sc = (torch.rand(64, generator=g) + 0.5).to(gpu)
     sh = torch.randn(64, generator=g).to(gpu)
     state = torch.zeros(C.fp8_state_floats(), device=gpu)
-    z, q = C.bn_act_fwd_q8(y, sc, sh, res, True, state, 0)
+    z, q, zm = C.bn_act_fwd_q8(y, sc, sh, res, True, state, 0, True)
     z_ref = C.bn_act_fwd(y, sc, sh, res, True)
     assert torch.equal(z, z_ref)
+    bits = (z.reshape(-1, 8) > 0).to(torch.int32) << torch.arange(8, device=gpu, dtype=torch.int32)
+    assert torch.equal(zm.to(torch.int32), bits.sum(1))
     assert torch.equal(_deq_e4m3(q), z.float().clamp(-448, 448).to(torch.float8_e4m3fn).float())
     torch.cuda.synchronize()
     D = C.fp8_deq_offset()

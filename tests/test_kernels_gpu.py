@@ -555,3 +555,28 @@ def test_fused_augment_matches_torch_loader(gpu, native_ext, normalized, augment
         assert torch.equal(ya, yb)
         assert xa.dtype == torch.float32 and xa.shape == xb.shape
         assert torch.equal(xa, xb)
+
+
+def test_relu_bitmask_dgrad_matches_z_mask(gpu, native_ext):
+    """bn_act_fwd_mask == bn_act_fwd + packed (z > 0) bits, and the BN-fused dgrad reading the
+    bits (mask 3) is bit-identical to reading z (mask 1)."""
+    C = native_ext
+    g = torch.Generator().manual_seed(31)
+    n, h, w_, c, k = 2, 14, 14, 256, 64
+    y = torch.randn(n, h, w_, c, generator=g).to(torch.bfloat16).to(gpu)
+    res = torch.randn(n, h, w_, c, generator=g).to(torch.bfloat16).to(gpu)
+    sc = (torch.rand(c, generator=g) + 0.5).to(gpu)
+    sh = torch.randn(c, generator=g).to(gpu)
+    z, zm = C.bn_act_fwd_mask(y, sc, sh, res)
+    assert torch.equal(z, C.bn_act_fwd(y, sc, sh, res, True))
+    bits = (z.reshape(-1, 8) > 0).to(torch.int32) << torch.arange(8, device=gpu, dtype=torch.int32)
+    assert torch.equal(zm.to(torch.int32), bits.sum(1))
+    dy = torch.randn(n, h, w_, k, generator=g).to(torch.bfloat16).to(gpu)
+    wt = (torch.randn(k, c, 1, 1, generator=g) * 0.05).to(gpu).contiguous(memory_format=torch.channels_last)
+    addend = torch.randn(n, h, w_, c, generator=g).to(torch.bfloat16).to(gpu)
+    stats = torch.stack([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5, sc.cpu(),
+                         sh.cpu()]).to(gpu)
+    g1, s1 = C.conv_dgrad_bn(dy, wt, [n, h, w_, c], 1, 0, addend, y, z, stats, 1)
+    g3, s3 = C.conv_dgrad_bn(dy, wt, [n, h, w_, c], 1, 0, addend, y, zm, stats, 3)
+    assert torch.equal(g1, g3)
+    assert torch.equal(s1, s3)
