@@ -23,7 +23,7 @@ namespace pdt {
 // stage 2: per channel sum over partitions, fixed order (deterministic).
 constexpr int FIN_CH = 32;
 constexpr int FIN_ROWS = 8;                 // threads per channel in a block
-constexpr int FIN_GPB = FIN_ROWS * 32;      // groups per block
+constexpr int FIN_GPB = FIN_ROWS * 16;      // groups per block (16 independent loads per thread)
 
 // Per-channel-tile completion counters for the single-launch two-level reductions below
 // (zero-initialised once; the last block of a tile resets its counter, so launches on one stream
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   float S = 0.f, A = 0.f, B = 0.f;
   if (mode != 2) {
   if (k < K) {
-#pragma unroll 4
+#pragma unroll 8
     for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
       const float cnt = (float)min(grows, M - g * grows);
       const float sg = part[((int64_t)g * 2 + 0) * K + k];
@@ -111,6 +111,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   const int P = mode == 2 ? nparts : gridDim.y;
   S = 0.f; A = 0.f; B = 0.f;
   if (k < K) {
+#pragma unroll 8
     for (int p = ty; p < P; p += FIN_ROWS) {
       const float* o = ws + ((int64_t)p * 3) * K;
       S += o[k]; A += o[K + k]; B += o[2 * K + k];
@@ -372,7 +373,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   float a = 0.f, b = 0.f;
   if (mode != 2) {
   if (k < K) {
-#pragma unroll 4
+#pragma unroll 8
     for (int g = g0 + ty; g < g1; g += FIN_ROWS) {
       a += part[((int64_t)g * 2 + 0) * K + k];
       b += part[((int64_t)g * 2 + 1) * K + k];
@@ -393,6 +394,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   const int P = mode == 2 ? nparts : gridDim.y;
   a = 0.f; b = 0.f;
   if (k < K) {
+#pragma unroll 8
     for (int p = ty; p < P; p += FIN_ROWS) {
       a += ws[(int64_t)p * 2 * K + k];
       b += ws[(int64_t)p * 2 * K + K + k];
