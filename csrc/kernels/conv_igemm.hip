@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace pdt {
@@ -465,86 +466,110 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   constexpr int IT_MAX = 4;  // 4 x (y, z, addend) chunks in flight: occupancy stays as without batching
   constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
   static_assert(IT_ALL % IT == 0, "chunk batches");
-  const bool has_add = P.addend != nullptr;
+  // The BN mask mode and the addend are wave-uniform: dispatch ONCE to a copy of the batch loop
+  // specialised on both (per-element tests of kernel arguments cost ~6x the SALU and 2.5x the
+  // VALU instructions of the plain epilogue, measured).
+  auto run_batches = [&](auto mm_c, auto ha_c) {
+    constexpr int MM = decltype(mm_c)::value;   // 0 none, 1 z > 0, 2 y*sc+sh > 0, 3 bitmask
+    constexpr bool HA = decltype(ha_c)::value;  // residual-gradient addend
 #pragma unroll 1
-  for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
-  uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
+    for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
+      uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int qd = lane + (b0 + it) * 64;
-    const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-    const int m = wrow0 + r;
-    const int col = wcol0 + c * 8;
-    ooff[it] = OOB;
-    if (m < P.M && col < P.Nout) {
-      int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
-      if (!P.dense) {    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
-        uint32_t n = fdiv((uint32_t)m, P.div_ij);
-        uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
-        uint32_t ii = fdiv(rem, P.div_j);
-        uint32_t jj = rem - ii * (uint32_t)P.Mj;
-        orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+      for (int it = 0; it < IT; ++it) {
+        const int qd = lane + (b0 + it) * 64;
+        const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+        const int m = wrow0 + r;
+        const int col = wcol0 + c * 8;
+        ooff[it] = OOB;
+        if (m < P.M && col < P.Nout) {
+          int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
+          if (!P.dense) {    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+            uint32_t n = fdiv((uint32_t)m, P.div_ij);
+            uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+            uint32_t ii = fdiv(rem, P.div_j);
+            uint32_t jj = rem - ii * (uint32_t)P.Mj;
+            orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+          }
+          ooff[it] = (uint32_t)((orow * P.Nout + col) * 2);
+        }
       }
-      ooff[it] = (uint32_t)((orow * P.Nout + col) * 2);
-    }
-  }
-  v4i av[IT], yv[IT], zv[IT];
-  if (has_add) {
-    const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.o_bytes);
+      v4i av[IT], yv[IT], zv[IT];
+      if constexpr (HA) {
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.o_bytes);
 #pragma unroll
-    for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, ooff[it]);
-  }
+        for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, ooff[it]);
+      }
+      if constexpr (EPI == EPI_BNB) {
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
+        if constexpr (MM == 1) {
+          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
+#pragma unroll
+          for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
+        } else if constexpr (MM == 3) {  // 1 byte per 16-B chunk instead of the 16-B z chunk
+          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes >> 4);
+#pragma unroll
+          for (int it = 0; it < IT; ++it)
+            zv[it][0] = (int)__builtin_amdgcn_raw_buffer_load_b8(rz, ooff[it] == OOB ? OOB : ooff[it] >> 4, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int qd = lane + (b0 + it) * 64;
+        const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+        v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+        if constexpr (HA) {  // fused residual-gradient sum (block input of a residual block)
+          f8 a = unpack8(__builtin_bit_cast(uint4, v));
+          const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
+          v = __builtin_bit_cast(v4i, pack8(a));
+        }
+        if constexpr (EPI == EPI_BNB) {
+          // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
+          // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
+          // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
+          f8 a = unpack8(__builtin_bit_cast(uint4, v));
+          const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
+          f8 zz;
+          if constexpr (MM == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
+          uint32_t zbits = 0u;
+          if constexpr (MM == 3) zbits = (uint32_t)zv[it][0];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            bool on = true;
+            if constexpr (MM == 1) on = zz.v[q] > 0.f;
+            if constexpr (MM == 2) on = fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f;
+            if constexpr (MM == 3) on = ((zbits >> q) & 1u) != 0u;
+            const float g = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
+            a.v[q] = g;
+            bsg[q] += g;
+            bsq[q] = fmaf(g, yy.v[q] - bmu[q], bsq[q]);
+          }
+          v = __builtin_bit_cast(v4i, pack8(a));
+        }
+        if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
+      }
+    }
+  };
+  using M0 = std::integral_constant<int, 0>;
+  using M1 = std::integral_constant<int, 1>;
+  using M2 = std::integral_constant<int, 2>;
+  using M3 = std::integral_constant<int, 3>;
+  using HT = std::integral_constant<bool, true>;
+  using HF = std::integral_constant<bool, false>;
+  const bool has_add = P.addend != nullptr;
   if constexpr (EPI == EPI_BNB) {
-    const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
-    if (P.bn_mask == 1) {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
-#pragma unroll
-      for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
-    } else if (P.bn_mask == 3) {  // 1 byte per 16-B chunk instead of the 16-B z chunk
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes >> 4);
-#pragma unroll
-      for (int it = 0; it < IT; ++it)
-        zv[it][0] = (int)__builtin_amdgcn_raw_buffer_load_b8(rz, ooff[it] == OOB ? OOB : ooff[it] >> 4, 0, 0);
+    switch (P.bn_mask) {
+      case 1: if (has_add) run_batches(M1{}, HT{}); else run_batches(M1{}, HF{}); break;
+      case 2: if (has_add) run_batches(M2{}, HT{}); else run_batches(M2{}, HF{}); break;
+      case 3: if (has_add) run_batches(M3{}, HT{}); else run_batches(M3{}, HF{}); break;
+      default: if (has_add) run_batches(M0{}, HT{}); else run_batches(M0{}, HF{}); break;
     }
-  }
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int qd = lane + (b0 + it) * 64;
-    const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-    v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
-    if (has_add) {  // fused residual-gradient sum (block input of a residual block)
-      f8 a = unpack8(__builtin_bit_cast(uint4, v));
-      const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
-      v = __builtin_bit_cast(v4i, pack8(a));
-    }
-    if constexpr (EPI == EPI_BNB) {
-      // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
-      // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
-      // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
-      f8 a = unpack8(__builtin_bit_cast(uint4, v));
-      const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
-      f8 zz;
-      if (P.bn_mask == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
-      const uint32_t zbits = P.bn_mask == 3 ? (uint32_t)zv[it][0] : 0u;
-      const bool valid = ooff[it] != OOB;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const bool on = valid && (P.bn_mask == 1 ? zz.v[q] > 0.f
-                                  : P.bn_mask == 3 ? ((zbits >> q) & 1u) != 0u
-                                  : (P.bn_mask == 2 ? fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f : true));
-        const float g = on ? a.v[q] : 0.f;
-        a.v[q] = g;
-        bsg[q] += g;
-        bsq[q] = fmaf(g, yy.v[q] - bmu[q], bsq[q]);
-      }
-      v = __builtin_bit_cast(v4i, pack8(a));
-    }
-    if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
-  }
+  } else {
+    if (has_add) run_batches(M0{}, HT{}); else run_batches(M0{}, HF{});
   }
   if constexpr (EPI == EPI_BNB) {
     // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the

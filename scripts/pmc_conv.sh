@@ -23,7 +23,7 @@ for shape in ${SHAPES:-256x14x14x256x3x3x1x1 64x56x56x64x3x3x1x1}; do
   for S in "$SET1" "$SET2" "$SET3" "$SET4" "$SET5"; do
     i=$((i+1))
     [ -z "$S" ] && continue
-    timeout -k 10 200 rocprofv3 --kernel-trace --pmc $S --output-format csv -d $O/${shape}_s$i -o run -- python3 $R/scripts/bench_conv.py --only $shape --iters 3 > $O/${shape}_s$i.log 2>&1
+    timeout -k 10 200 rocprofv3 --kernel-trace --pmc $S --output-format csv -d $O/${shape}_s$i -o run -- python3 $R/scripts/bench_conv.py --only $shape --iters 3 $BENCH_ARGS > $O/${shape}_s$i.log 2>&1
     rc=$?; echo "$shape set$i rc=$rc" >> $O/status.txt
     [ $rc -eq 0 ] || exit $rc
   done
