@@ -178,6 +178,12 @@ class ResNet(nn.Module):
         return self.fc(x)
 
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:  # every BN counter bumped by one launch (see ops.bump_bn_counters)
+            with ops.bump_bn_counters(self):
+                return self._forward_native(x)
+        return self._forward_native(x)
+
+    def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
         # NCHW fp32 image (or an NHWC bf16 tensor already prepared by the data
         # pipeline) -> NHWC bf16 with C padded to the kernels' 8-channel granule.
         if x.is_cuda:  # bf16 conv-weight mirror of the DDP flat space (refreshed if stale)

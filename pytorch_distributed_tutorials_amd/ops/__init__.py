@@ -9,6 +9,7 @@ from .fused import (  # noqa: F401
     CrossEntropyLoss,
     act_dtype,
     avgpool_linear,
+    bump_bn_counters,
     conv_bn,
     cross_entropy,
     fp8_attach,

@@ -292,16 +292,10 @@ def conv_bn(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool,
     """z = act(BN(conv(x)) [+ residual]) on NHWC activations."""
     stride = conv.stride[0]
     pad = conv.padding[0]
-    training = bn.training or not bn.track_running_stats
-    momentum = bn.momentum
-    if training and bn.track_running_stats:
-        with torch.no_grad():
-            bn.num_batches_tracked.add_(1)
-        if momentum is None:  # cumulative moving average (torch BN semantics)
-            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    training, momentum, eps = _bn_prepare(bn)
     return _ConvBN.apply(x, conv.weight, bn.weight, bn.bias, residual,
                          bn.running_mean, bn.running_var, stride, pad, relu,
-                         training, momentum if momentum is not None else 0.0, bn.eps)
+                         training, momentum, eps)
 
 
 # ----------------------------------------------------------------------------
@@ -407,11 +401,39 @@ def top1_correct(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 # whole residual block (device path): one autograd node per Bottleneck/BasicBlock
 # ----------------------------------------------------------------------------
+_NBT_BATCHED = 0  # > 0 inside bump_bn_counters(): the counters were already bumped in one launch
+
+
+class bump_bn_counters:
+    """Context for one device forward of a whole model: bumps every training BatchNorm's
+    ``num_batches_tracked`` (torch BN semantics) with ONE multi-tensor launch
+    instead of one ``add_`` kernel per BN (53 launches per ResNet-50 step); the per-BN
+    ``_bn_prepare`` calls inside the context then skip their own bump."""
+
+    def __init__(self, module: nn.Module):
+        self.counters = [m.num_batches_tracked for m in module.modules()
+                         if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.training
+                         and m.track_running_stats and m.num_batches_tracked is not None]
+
+    def __enter__(self):
+        global _NBT_BATCHED
+        if self.counters:
+            with torch.no_grad():
+                torch._foreach_add_(self.counters, 1)
+        _NBT_BATCHED += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _NBT_BATCHED
+        _NBT_BATCHED -= 1
+        return False
+
+
 def _bn_prepare(bn: nn.BatchNorm2d):
     """(training, momentum, eps) for one BN call; bumps num_batches_tracked like torch."""
     training = bn.training or not bn.track_running_stats
     momentum = bn.momentum
-    if training and bn.track_running_stats:
+    if training and bn.track_running_stats and not _NBT_BATCHED:
         with torch.no_grad():
             bn.num_batches_tracked.add_(1)
         if momentum is None:
