@@ -242,15 +242,28 @@ void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift
 }
 
 // ------------------------------------------------------------ backward reduce
-// Block b reduces rows [b*RPB, (b+1)*RPB) for all channels; requires 256 % K8 == 0.
+// Block (bx, by) reduces rows [bx*RPB, (bx+1)*RPB) of channel chunk by (<= RED_CH8 8-channel
+// groups = 256 channels).  Chunking the channels keeps >= 8 rows in flight per iteration and
+// gives wide layers (K = 1024/2048 at M = 50176/12544) a grid that fills the chip: with all K
+// channels in one block a 2048-channel reduction ran on 49 blocks at ~0.5 TB/s.
 constexpr int RED_BLOCKS_MAX = 1024;
+constexpr int RED_CH8 = 32;
+constexpr int RED_TARGET = 2048;  // blocks per launch (8 per CU)
 
-static int red_blocks(int64_t M) {
-  int64_t b = (M + 255) / 256;  // >= 256 rows per block
-  return (int)(b < RED_BLOCKS_MAX ? b : RED_BLOCKS_MAX);
+static int red_chunks(int K) {
+  const int K8 = K / 8;
+  return K8 > RED_CH8 ? K8 / RED_CH8 : 1;
 }
 
-size_t bn_bwd_ws_floats(int64_t M, int K) { return (size_t)red_blocks(M) * 2 * K; }
+static int red_blocks(int64_t M, int K) {
+  const int64_t by_rows = (M + 31) / 32;  // >= 32 rows per block
+  int64_t b = (RED_TARGET + red_chunks(K) - 1) / red_chunks(K);
+  b = std::max<int64_t>(b, (M + 1023) / 1024);  // <= 1024 rows per block
+  b = std::min<int64_t>(std::min<int64_t>(b, by_rows), RED_BLOCKS_MAX);
+  return (int)std::max<int64_t>(b, 1);
+}
+
+size_t bn_bwd_ws_floats(int64_t M, int K) { return (size_t)red_blocks(M, K) * 2 * K; }
 
 // Relu-mask modes of the backward kernels: 0 = no ReLU, 1 = mask from the saved output z (z > 0),
 // 2 = mask recomputed from y (y*scale + shift > 0, bit-identical to the forward's fp32 math) --
@@ -278,10 +291,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
                                                             float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int K = K8 * 8;
+  const int CH8 = K8 < RED_CH8 ? K8 : RED_CH8;  // 8-channel groups of this block's chunk
   const int t = threadIdx.x;
-  const int c8 = t % K8;
-  const int rpi = 256 / K8;  // rows per iteration
-  const int roff = t / K8;
+  const int c8 = blockIdx.y * CH8 + t % CH8;
+  const int rpi = 256 / CH8;  // rows per iteration
+  const int roff = t / CH8;
   int64_t rows_per_block = (M + gridDim.x - 1) / gridDim.x;
   int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   int64_t r1 = min(M, r0 + rows_per_block);
@@ -310,7 +324,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
   __syncthreads();
   for (int s = rpi / 2; s > 0; s >>= 1) {
     if (roff < s) {
-      float* o = sh + (size_t)(t + s * K8) * 16;
+      float* o = sh + (size_t)(t + s * CH8) * 16;
 #pragma unroll
       for (int j = 0; j < 16; ++j) my[j] += o[j];
     }
@@ -419,17 +433,20 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
                               const float* stats, int mask, int64_t M, int K, float* ws,
                               float* sums, float* dgamma, float* dbeta, hipStream_t st) {
   int K8 = K / 8;
-  int nb = red_blocks(M);
+  if (K8 > RED_CH8 ? (K8 % RED_CH8 != 0) : (256 % K8 != 0))
+    throw std::runtime_error("bn_act_bwd_reduce: channel count not supported");
+  int nb = red_blocks(M, K);
+  dim3 grid(nb, red_chunks(K));
   size_t shmem = 256 * 16 * sizeof(float);
   auto DZ = reinterpret_cast<const uint4*>(dz);
   auto Z = reinterpret_cast<const uint4*>(z);
   auto Y = reinterpret_cast<const uint4*>(y);
   if (mask == 1)
-    hipLaunchKernelGGL(bn_bwd_reduce_stage1<1>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<1>, grid, dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
   else if (mask == 2)
-    hipLaunchKernelGGL(bn_bwd_reduce_stage1<2>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<2>, grid, dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_stage1<0>, dim3(nb), dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
+    hipLaunchKernelGGL(bn_bwd_reduce_stage1<0>, grid, dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
   hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K, sums,
                      stats + K, dgamma, dbeta);
 }

@@ -121,11 +121,15 @@ def test_conv_wgrad(gpu, native_ext, shape, deterministic):
     assert _rel_err(dw, dwr) < 1e-2
 
 
-@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
-def test_bn_act_fwd_bwd(gpu, native_ext, relu, res):
+@pytest.mark.parametrize("relu,res,nhwk", [
+    (True, False, (4, 7, 9, 128)), (True, True, (4, 7, 9, 128)), (False, False, (4, 7, 9, 128)),
+    # channel-chunked reduction grid (K8 > 32) and a many-row-block case
+    (False, False, (16, 7, 7, 2048)), (True, True, (8, 14, 14, 512)), (True, False, (64, 28, 28, 64)),
+])
+def test_bn_act_fwd_bwd(gpu, native_ext, relu, res, nhwk):
     C = native_ext
     g = torch.Generator().manual_seed(11)
-    n, h, w, k = 4, 7, 9, 128
+    n, h, w, k = nhwk
     y = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
     r = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu) if res else None
     gamma = (torch.rand(k, generator=g) + 0.5).to(gpu)
@@ -136,7 +140,7 @@ def test_bn_act_fwd_bwd(gpu, native_ext, relu, res):
     shift = beta - mean * scale
     z = C.bn_act_fwd(y, scale, shift, r, relu)
     zr = ref.bn_act_fwd(y, mean, invstd, gamma, beta, r, relu, torch.float32)
-    assert (z.float() - zr).abs().max().item() < 3e-2
+    assert ((z.float() - zr).abs() / zr.abs().clamp_min(1.0)).max().item() < 1.6e-2  # bf16 output
     stats = torch.stack([mean, invstd, scale, shift]).contiguous()
     dz = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
     dyr, dgr, dbr, dresr = ref.bn_act_bwd(dz, z, y, mean, invstd, gamma, relu, True, res, torch.float32)
