@@ -303,6 +303,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
   load8(stats + c8 * 8, mu);
   if (MASK == 2) { load8(stats + 2 * K + c8 * 8, sc); load8(stats + 3 * K + c8 * 8, shf); }
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
   for (int64_t r = r0 + roff; r < r1; r += rpi) {
     int64_t v = r * K8 + c8;
     f8 d = unpack8(dz[v]);
@@ -337,20 +338,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
   }
 }
 
-// block = 32 channels x 8 partial-lanes; each lane sums nb/8 stage-1 partials (independent
-// loads, pipelined), then an LDS combine.  Deterministic (fixed order).
+// block = CH channels x (256/CH) partial-lanes; each lane sums its share of the nb stage-1
+// partials (independent loads, pipelined), then an LDS combine.  Deterministic (fixed order).
+// CH = 32 for wide layers; CH = 8 when K/32 blocks would leave most of the chip idle.
+template <int CH>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restrict__ ws, int nb,
                                                             int K, float* __restrict__ sums,
                                                             const float* __restrict__ invstd,
                                                             float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta) {
-  __shared__ float sa[8][33], sb[8][33];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int k = blockIdx.x * 32 + tx;
+  constexpr int L = 256 / CH;
+  __shared__ float sa[L][CH + 1], sb[L][CH + 1];
+  const int tx = threadIdx.x % CH, ty = threadIdx.x / CH;
+  const int k = blockIdx.x * CH + tx;
   float a = 0.f, b = 0.f;
   if (k < K) {
 #pragma unroll 4
-    for (int i = ty; i < nb; i += 8) {
+    for (int i = ty; i < nb; i += L) {
       a += ws[(int64_t)i * 2 * K + k];
       b += ws[(int64_t)i * 2 * K + K + k];
     }
@@ -359,7 +363,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage2(const float* __restr
   sb[ty][tx] = b;
   __syncthreads();
   if (ty == 0 && k < K) {
-    for (int r = 1; r < 8; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
+    for (int r = 1; r < L; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
     sums[k] = a;       // sum g          (= dbeta)
     sums[K + k] = b;   // sum g*(y-mean) (dgamma = b*invstd)
     if (dgamma != nullptr) {
@@ -447,8 +451,12 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
     hipLaunchKernelGGL(bn_bwd_reduce_stage1<2>, grid, dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_stage1<0>, grid, dim3(256), shmem, st, DZ, Z, Y, stats, M, K8, ws);
-  hipLaunchKernelGGL(bn_bwd_reduce_stage2, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K, sums,
-                     stats + K, dgamma, dbeta);
+  if (K >= 1024)
+    hipLaunchKernelGGL(bn_bwd_reduce_stage2<32>, dim3(ceil_div(K, 32)), dim3(256), 0, st, ws, nb, K,
+                       sums, stats + K, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_stage2<8>, dim3(ceil_div(K, 8)), dim3(256), 0, st, ws, nb, K,
+                       sums, stats + K, dgamma, dbeta);
 }
 
 // ------------------------------------------------------------- backward apply

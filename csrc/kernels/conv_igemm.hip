@@ -606,6 +606,7 @@ struct TnArgs {
   int HoWo, Wo;
   int steps_per_split, nsteps;
   int accumulate;      // single-split direct store: out += acc instead of out = acc
+  int staged;          // epilogue through the LDS row image (256-B segments); 0 = direct (A/B knob)
 };
 
 // LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
@@ -830,6 +831,42 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
   // otherwise a private fp32 [Kout][Ncols] slab per split, summed by splitk_reduce_kernel.
   const int fq = lane >> 4, fr = lane & 15;
   float* o = ATOMIC ? P.out : P.out + (int64_t)split * P.Kout * P.Ncols;
+  // Staged form: the 16x16 accumulator layout gives every store / atomic wave-instruction four
+  // 64-B row pieces; through a wave-private row-major LDS image (the drained pipeline buffers:
+  // every DMA landed and every wave passed the loop's last barrier) each instruction instead
+  // covers one 256-B segment of a dW row, the shape float atomics run at full rate
+  // (MI355X_MICROARCH "Global float atomics").  Column XOR 16 on rows 4..7 mod 8 keeps both the
+  // fragment writes (lanes fq=0/1 are 4 rows apart) and the row reads conflict-free.
+  constexpr bool STAGED = TN * 16 == 64 && CFG::WAVES * TM * 16 * 64 * 4 <= CFG::SMEM;
+  if (STAGED && P.staged) {
+    float* stg = reinterpret_cast<float*>(smem) + wid * (TM * 16) * 64;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = i * 16 + fq * 4 + e;
+          stg[r * 64 + ((j * 16 + fr) ^ (((r >> 2) & 1) << 4))] = acc[i][j][e];
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the region is wave-private
+    __builtin_amdgcn_wave_barrier();
+    const int col = c0 + wn * 64 + lane;
+    const int row0 = k0 + wm * TM * 16;
+    if (col < P.Ncols) {
+#pragma unroll 8
+      for (int r = 0; r < TM * 16; ++r) {
+        const float v = stg[r * 64 + (lane ^ (((r >> 2) & 1) << 4))];
+        if (row0 + r < P.Kout) {
+          float* dst = o + (int64_t)(row0 + r) * P.Ncols + col;
+          if (ATOMIC) unsafeAtomicAdd(dst, v);
+          else if (P.accumulate) *dst += v;
+          else *dst = v;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1143,7 +1180,16 @@ static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
   // bound the reduction traffic: atomics/slabs move splits * |dW| * 4 bytes
   const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
-  const int64_t cap_bytes = deterministic ? ((int64_t)64 << 20) : ((int64_t)32 << 20);
+  // PDT_WGRAD_CAP_MB="<atomic>,<slab>" overrides the reduction-traffic caps (tuning knob)
+  static int64_t cap_atomic = -1, cap_slab = -1;
+  if (cap_atomic < 0) {
+    cap_atomic = 32; cap_slab = 64;
+    if (const char* e = getenv("PDT_WGRAD_CAP_MB")) {
+      int a = 0, b = 0;
+      if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) { cap_atomic = a; cap_slab = b; }
+    }
+  }
+  const int64_t cap_bytes = (deterministic ? cap_slab : cap_atomic) << 20;
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, cap_bytes / dw_bytes));
   splits = std::max(1, std::min(splits, 256));
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
@@ -1190,6 +1236,12 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.steps_per_split = p.steps_per_split;
   a.nsteps = p.nsteps;
   a.accumulate = (accumulate && !slab) ? 1 : 0;  // slabs are private partials: always overwritten
+  static int staged = -1;
+  if (staged < 0) {
+    const char* e = getenv("PDT_TN_STAGED");
+    staged = (e && e[0] == '0') ? 0 : 1;
+  }
+  a.staged = staged;
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;

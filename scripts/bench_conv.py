@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--only", default=None, help="single shape CxHxWxKxRxSxstridexpad")
     ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3) forward conv")
     ap.add_argument("--bn", action="store_true", help="also time dgrad with the fused BN-backward epilogue")
+    ap.add_argument("--det", action="store_true", help="wgrad in deterministic mode (split-K slabs + reduce)")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda:0")
@@ -95,7 +96,7 @@ def main():
         flop = 2.0 * N * ho * wo * k * c * r * s
         f = timeit(lambda: C.conv_fwd(x, wk, st, pd, True), a.iters)
         d = timeit(lambda: C.conv_dgrad(dy, wt, [N, h, w, c], st, pd), a.iters) if c % 8 == 0 else 0.0
-        g = timeit(lambda: C.conv_wgrad(dy, x, [k, c, r, s], st, pd, False), a.iters)
+        g = timeit(lambda: C.conv_wgrad(dy, x, [k, c, r, s], st, pd, a.det), a.iters)
         row = [c, h, w, k, r, s, st, pd, cnt, N * ho * wo, k, c * r * s,
                round(f, 3), round(flop / f / 1e9, 1), round(d, 3), round(flop / d / 1e9, 1) if d else 0,
                round(g, 3), round(flop / g / 1e9, 1)]
