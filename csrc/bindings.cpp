@@ -640,6 +640,72 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, int64_t H, int64_t W) {
   return dx;
 }
 
+// stem: (pooled, idx) = maxpool3x3s2(relu(y*scale + shift)) without writing the ReLU output
+std::tuple<Tensor, Tensor> bn_relu_maxpool(const Tensor& y, const Tensor& scale, const Tensor& shift) {
+  check_bf16_nhwc(y, "y");
+  check_cuda(scale, "scale");
+  check_cuda(shift, "shift");
+  c10::hip::HIPGuard g(y.get_device());
+  int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat &&
+              shift.scalar_type() == at::kFloat, "scale/shift must be fp32 [C]");
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  auto out = at::empty({N, Ho, Wo, C}, y.options());
+  auto idx = at::empty({N, Ho, Wo, C}, y.options().dtype(at::kByte));
+  pdt::launch_bn_relu_maxpool(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), bf(out),
+                              idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, cur_stream(y));
+  return {out, idx};
+}
+
+static void check_pool_grad(const Tensor& dpool, const Tensor& idx, const Tensor& y) {
+  check_bf16_nhwc(dpool, "dpool");
+  check_bf16_nhwc(y, "y");
+  check_cuda(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.sizes() == dpool.sizes(), "idx must be uint8 like dpool");
+  TORCH_CHECK(dpool.size(0) == y.size(0) && dpool.size(3) == y.size(3) &&
+              dpool.size(1) == (y.size(1) - 1) / 2 + 1 && dpool.size(2) == (y.size(2) - 1) / 2 + 1,
+              "dpool must be the 3x3/s2/p1 max pool of y");
+}
+
+// sums[2][K] of the stem BN backward with dz = maxpool_bwd(dpool, idx) gathered on the fly
+Tensor pool_bn_bwd_reduce(const Tensor& dpool, const Tensor& idx, const Tensor& y, const Tensor& stats,
+                          const std::optional<Tensor>& dgamma, const std::optional<Tensor>& dbeta) {
+  check_pool_grad(dpool, idx, y);
+  c10::hip::HIPGuard g(y.get_device());
+  int N = y.size(0), H = y.size(1), W = y.size(2), K = y.size(3);
+  TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
+  auto fopt = y.options().dtype(at::kFloat);
+  auto ws = at::empty({(int64_t)pdt::pool_bn_bwd_ws_floats((int64_t)N * H * W, K)}, fopt);
+  auto sums = at::empty({2, K}, fopt);
+  float* dg = nullptr;
+  float* db = nullptr;
+  if (dgamma.has_value() && dgamma->defined()) {
+    TORCH_CHECK(dbeta.has_value() && dbeta->defined(), "dgamma and dbeta go together");
+    TORCH_CHECK(dgamma->numel() == K && dbeta->numel() == K && dgamma->is_contiguous() &&
+                dbeta->is_contiguous() && dgamma->scalar_type() == at::kFloat, "bad dgamma/dbeta");
+    dg = dgamma->data_ptr<float>();
+    db = dbeta->data_ptr<float>();
+  }
+  pdt::launch_pool_bn_bwd_reduce(cbf(dpool), idx.data_ptr<uint8_t>(), cbf(y), stats.data_ptr<float>(), N, H,
+                                 W, K, dpool.size(1), dpool.size(2), ws.data_ptr<float>(),
+                                 sums.data_ptr<float>(), dg, db, cur_stream(y));
+  return sums;
+}
+
+Tensor pool_bn_bwd_apply(const Tensor& dpool, const Tensor& idx, const Tensor& y, const Tensor& stats,
+                         const Tensor& gamma, const Tensor& sums, bool training) {
+  check_pool_grad(dpool, idx, y);
+  c10::hip::HIPGuard g(y.get_device());
+  int N = y.size(0), H = y.size(1), W = y.size(2), K = y.size(3);
+  TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
+  TORCH_CHECK(sums.numel() == 2 * K && gamma.numel() == K, "sums [2, K] / gamma [K]");
+  auto dy = at::empty_like(y);
+  pdt::launch_pool_bn_bwd_apply(cbf(dpool), idx.data_ptr<uint8_t>(), cbf(y), stats.data_ptr<float>(),
+                                gamma.data_ptr<float>(), sums.data_ptr<float>(), training, N, H, W, K,
+                                dpool.size(1), dpool.size(2), bf(dy), cur_stream(y));
+  return dy;
+}
+
 Tensor avgpool_fwd(const Tensor& x) {
   check_bf16_nhwc(x, "x");
   c10::hip::HIPGuard g(x.get_device());
@@ -879,6 +945,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("flip"), py::arg("pad"), py::arg("normalize"), py::arg("mean"), py::arg("std"));
   m.def("maxpool_fwd", checked("maxpool_fwd", &maxpool_fwd));
   m.def("maxpool_bwd", checked("maxpool_bwd", &maxpool_bwd));
+  m.def("bn_relu_maxpool", checked("bn_relu_maxpool", &bn_relu_maxpool));
+  m.def("pool_bn_bwd_reduce", checked("pool_bn_bwd_reduce", &pool_bn_bwd_reduce), py::arg("dpool"),
+        py::arg("idx"), py::arg("y"), py::arg("stats"), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
+  m.def("pool_bn_bwd_apply", checked("pool_bn_bwd_apply", &pool_bn_bwd_apply));
   m.def("avgpool_fwd", checked("avgpool_fwd", &avgpool_fwd));
   m.def("avgpool_bwd", checked("avgpool_bwd", &avgpool_bwd));
   m.def("softmax_xent", checked("softmax_xent", &softmax_xent));

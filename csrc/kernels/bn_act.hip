@@ -591,4 +591,235 @@ void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float
   }
 }
 
+
+// ---------------------------------------------- stem: BN + ReLU + 3x3/s2/p1 max pool, fused
+// Forward: every window element is normalised, ReLU'd and rounded to bf16 exactly as bn_act_fwd
+// would store it, then max-pooled in registers (same first-maximum tie rule as maxpool_fwd):
+// the full-resolution z (411 MB at batch 256) is never written nor read back.  Backward: the
+// pooled gradient is gathered back to the full-resolution position inside the BN reduction and
+// apply passes (pool_grad8, the maxpool_bwd gather), so dz is never materialised either.
+// The ReLU mask is recomputed from y (mode 2).  Requires K8 <= 32 and 256 % K8 == 0.
+__device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
+
+__device__ __forceinline__ f8 pool_grad8(const uint4* __restrict__ dp, const uint2* __restrict__ idx,
+                                         int n, int h, int w, int c8, int C8, int Ho, int Wo) {
+  f8 acc;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc.v[j] = 0.f;
+  const int ho0 = h >> 1, ho1 = min((h + 1) >> 1, Ho - 1);
+  const int wo0 = w >> 1, wo1 = min((w + 1) >> 1, Wo - 1);
+  for (int ho = ho0; ho <= ho1; ++ho) {
+    const int kh = h - (ho * 2 - 1);
+    for (int wo = wo0; wo <= wo1; ++wo) {
+      const uint32_t pos = (uint32_t)(kh * 3 + (w - (wo * 2 - 1)));
+      const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C8 + c8;
+      const uint2 id = idx[o];
+      const f8 g = unpack8(dp[o]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t b = ((j < 4 ? id.x : id.y) >> (8 * (j & 3))) & 0xffu;
+        if (b == pos) acc.v[j] += g.v[j];
+      }
+    }
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __restrict__ y,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              uint4* __restrict__ out,
+                                                              uint2* __restrict__ idx, int N, int H,
+                                                              int W, int C8, int Ho, int Wo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  if (t >= total) return;
+  const int c8 = (int)(t % C8);
+  const int64_t p = t / C8;
+  const int wo = (int)(p % Wo);
+  const int64_t q = p / Wo;
+  const int ho = (int)(q % Ho);
+  const int n = (int)(q / Ho);
+  float sc[8], sh[8];
+  load8(scale + c8 * 8, sc);
+  load8(shift + c8 * 8, sh);
+  float best[8];
+  uint32_t bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = ho * 2 - 1 + kh;
+    if (h < 0 || h >= H) continue;
+    for (int kw = 0; kw < 3; ++kw) {
+      const int w = wo * 2 - 1 + kw;
+      if (w < 0 || w >= W) continue;
+      const f8 v = unpack8(y[(((int64_t)n * H + h) * W + w) * C8 + c8]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float z = bf16_round(fmaxf(fmaf(v.v[j], sc[j], sh[j]), 0.f));
+        if (z > best[j] || __builtin_isnan(z)) { best[j] = z; bi[j] = (uint32_t)(kh * 3 + kw); }
+      }
+    }
+  }
+  f8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = best[j];
+  out[t] = pack8(o);
+  idx[t] = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                      bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+}
+
+// stage 1 of the stem BN backward reduction with dz gathered from the pooled gradient
+__global__ void __launch_bounds__(256) pool_bn_bwd_reduce_kernel(const uint4* __restrict__ dp,
+                                                                 const uint2* __restrict__ idx,
+                                                                 const uint4* __restrict__ y,
+                                                                 const float* __restrict__ stats,
+                                                                 int64_t M, int K8, int H, int W,
+                                                                 int Ho, int Wo, float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int K = K8 * 8;
+  const int t = threadIdx.x;
+  const int c8 = t % K8;
+  const int rpi = 256 / K8;
+  const int roff = t / K8;
+  const int64_t rows_per_block = (M + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float mu[8], sc[8], shf[8];
+  load8(stats + c8 * 8, mu);
+  load8(stats + 2 * K + c8 * 8, sc);
+  load8(stats + 3 * K + c8 * 8, shf);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int HW = H * W;
+#pragma unroll 2
+  for (int64_t r = r0 + roff; r < r1; r += rpi) {
+    const int n = (int)(r / HW);
+    const int rem = (int)(r - (int64_t)n * HW);
+    const int h = rem / W, w = rem - (rem / W) * W;
+    const f8 d = pool_grad8(dp, idx, n, h, w, c8, K8, Ho, Wo);
+    const f8 yy = unpack8(y[r * K8 + c8]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = relu_grad<2>(d.v[j], 0.f, yy.v[j], sc[j], shf[j]);
+      sg[j] += g;
+      sgx[j] = fmaf(g, yy.v[j] - mu[j], sgx[j]);
+    }
+  }
+  float* my = sh + (size_t)t * 16;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { my[j] = sg[j]; my[8 + j] = sgx[j]; }
+  __syncthreads();
+  for (int s = rpi / 2; s > 0; s >>= 1) {
+    if (roff < s) {
+      const float* o = sh + (size_t)(t + s * K8) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) my[j] += o[j];
+    }
+    __syncthreads();
+  }
+  if (roff == 0) {
+    float* o = ws + (int64_t)blockIdx.x * 2 * K;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = my[j]; o[K + c8 * 8 + j] = my[8 + j]; }
+  }
+}
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) pool_bn_bwd_apply_kernel(
+    const uint4* __restrict__ dp, const uint2* __restrict__ idx, const uint4* __restrict__ y,
+    const float* __restrict__ stats, const float* __restrict__ gamma, const float* __restrict__ sums,
+    int64_t nvec, int K8, int H, int W, int Ho, int Wo, float invM, uint4* __restrict__ dy) {
+  const int K = K8 * 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = (int)(tid % K8);
+  const int c0 = c8 * 8;
+  float k1[8], sgm[8], k2[8], mu[8], sc[8], shf[8];
+  {
+    float is[8], gm[8], s0[8], s1[8];
+    load8(stats + K + c0, is);
+    load8(gamma + c0, gm);
+    load8(stats + c0, mu);
+    load8(sums + c0, s0);
+    load8(sums + K + c0, s1);
+    load8(stats + 2 * K + c0, sc);
+    load8(stats + 3 * K + c0, shf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k1[j] = gm[j] * is[j];
+      sgm[j] = s0[j] * invM;
+      k2[j] = s1[j] * is[j] * is[j] * invM;
+    }
+  }
+  const int HW = H * W;
+  for (int64_t v = tid; v < nvec; v += stride) {
+    const int64_t r = v / K8;
+    const int n = (int)(r / HW);
+    const int rem = (int)(r - (int64_t)n * HW);
+    const int h = rem / W, w = rem - (rem / W) * W;
+    const f8 d = pool_grad8(dp, idx, n, h, w, c8, K8, Ho, Wo);
+    const f8 yy = unpack8(y[v]);
+    f8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = relu_grad<2>(d.v[j], 0.f, yy.v[j], sc[j], shf[j]);
+      o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
+    }
+    dy[v] = pack8(o);
+  }
+}
+
+static void check_pool_bn_channels(int K) {
+  const int K8 = K / 8;
+  if (K % 8 != 0 || K8 > 32 || 256 % K8 != 0)
+    throw std::runtime_error("fused BN + max pool: channels must be 8..256 and divide 2048");
+}
+
+void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* shift, uint16_t* out,
+                            uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
+  check_pool_bn_channels(C);
+  const int C8 = C / 8;
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint4*>(y), scale, shift, reinterpret_cast<uint4*>(out),
+                     reinterpret_cast<uint2*>(idx), N, H, W, C8, Ho, Wo);
+}
+
+size_t pool_bn_bwd_ws_floats(int64_t M, int K) { return bn_bwd_ws_floats(M, K); }
+
+void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
+                               const float* stats, int N, int H, int W, int K, int Ho, int Wo,
+                               float* ws, float* sums, float* dgamma, float* dbeta, hipStream_t st) {
+  check_pool_bn_channels(K);
+  const int K8 = K / 8;
+  const int64_t M = (int64_t)N * H * W;
+  const int nb = red_blocks(M, K);
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 256 * 16 * sizeof(float), st,
+                     reinterpret_cast<const uint4*>(dpool), reinterpret_cast<const uint2*>(idx),
+                     reinterpret_cast<const uint4*>(y), stats, M, K8, H, W, Ho, Wo, ws);
+  hipLaunchKernelGGL(bn_bwd_reduce_stage2<8>, dim3(ceil_div(K, 8)), dim3(256), 0, st, ws, nb, K, sums,
+                     stats + K, dgamma, dbeta);
+}
+
+void launch_pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
+                              const float* stats, const float* gamma, const float* sums, bool training,
+                              int N, int H, int W, int K, int Ho, int Wo, uint16_t* dy, hipStream_t st) {
+  check_pool_bn_channels(K);
+  const int K8 = K / 8;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t nvec = M * K8;
+  dim3 g(ew_blocks(nvec)), b(256);
+  const float invM = 1.f / (float)M;
+  auto DP = reinterpret_cast<const uint4*>(dpool);
+  auto ID = reinterpret_cast<const uint2*>(idx);
+  auto Y = reinterpret_cast<const uint4*>(y);
+  auto DY = reinterpret_cast<uint4*>(dy);
+  if (training)
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<true>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvec,
+                       K8, H, W, Ho, Wo, invM, DY);
+  else
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<false>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvec,
+                       K8, H, W, Ho, Wo, invM, DY);
+}
+
 }  // namespace pdt

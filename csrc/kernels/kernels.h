@@ -113,6 +113,19 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
                              bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
                              hipStream_t st);
 
+// Stem BN + ReLU + 3x3/s2/p1 max pool fused (bn_act.hip): out/idx as maxpool_fwd of the ReLU'd
+// bf16 z, which is never written.  Backward: the BN reduction / apply with dz gathered from the
+// pooled gradient (mask mode 2); ws >= pool_bn_bwd_ws_floats(N*H*W, K).  K <= 256.
+void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* shift, uint16_t* out,
+                            uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
+size_t pool_bn_bwd_ws_floats(int64_t M, int K);
+void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
+                               const float* stats, int N, int H, int W, int K, int Ho, int Wo,
+                               float* ws, float* sums, float* dgamma, float* dbeta, hipStream_t st);
+void launch_pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
+                              const float* stats, const float* gamma, const float* sums, bool training,
+                              int N, int H, int W, int K, int Ho, int Wo, uint16_t* dy, hipStream_t st);
+
 // ---------------------------------------------------------------- pool.hip
 void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C,
                         int Ho, int Wo, hipStream_t st);

@@ -192,12 +192,13 @@ class ResNet(nn.Module):
             if mirror is not None:
                 mirror.ensure()
         if x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and x.is_floating_point():
-            x = ops.stem_conv_bn(x, self.conv1, self.bn1)  # super-pixel stem (fused.py)
+            # super-pixel stem conv, then BN + ReLU + max pool in one pass (fused.py)
+            x = ops.stem_conv_bn_pool(x, self.conv1, self.bn1, self.maxpool)
         else:
             if x.dim() == 4 and x.shape[1] == 3:
                 x = ops.image_to_nhwc(x)
             x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
-        x = ops.maxpool3x3s2(x)
+            x = ops.maxpool3x3s2(x)
         x = ops.fp8_attach(x, self.maxpool)  # e4m3 copy for fp8 convs (no-op unless ops.set_fp8)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

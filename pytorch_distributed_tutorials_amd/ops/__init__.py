@@ -20,5 +20,6 @@ from .fused import (  # noqa: F401
     set_fp8,
     set_cpu_activation_dtype,
     stem_conv_bn,
+    stem_conv_bn_pool,
     top1_correct,
 )

@@ -276,11 +276,87 @@ class _StemConvBN(torch.autograd.Function):
                 None, None, None)
 
 
+class _StemConvBNPool(torch.autograd.Function):
+    """_StemConvBN followed by the 3x3/s2/p1 max pool in ONE fused BN-apply/ReLU/pool pass.
+
+    The full-resolution ReLU output (112x112x64 per image) is never written: forward normalises,
+    rectifies and pools each window in registers (``bn_relu_maxpool``), backward gathers the
+    pooled gradient back through the argmax inside the BN reduction and apply passes
+    (``pool_bn_bwd_reduce`` / ``pool_bn_bwd_apply``).  Saves writing z and dz and reading each
+    of them back (~1.6 GB of HBM traffic per step at batch 256).
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, pad, training,
+                momentum, eps):
+        C = native()
+        xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
+        k = weight.shape[0]
+        count = y.shape[0] * y.shape[1] * y.shape[2]
+        if training:
+            if running_mean is None:
+                running_mean = torch.zeros(k, device=x.device)
+                running_var = torch.ones(k, device=x.device)
+            stats = C.bn_finalize(part, count, running_mean, running_var, gamma, beta,
+                                  float(momentum), float(eps))
+        else:
+            stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
+        out, idx = C.bn_relu_maxpool(y, stats[2], stats[3])
+        _nan_trace("stem+pool", x=x, xsp=xsp, y=y, part=part, stats=stats, out=out)
+        ctx.save_for_backward(xsp, y, stats, gamma, idx)
+        ctx.weight = weight
+        ctx.training = training
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = native()
+        xsp, y, stats, gamma, idx = ctx.saved_tensors
+        weight = ctx.weight
+        dout = dout.contiguous()
+        sums = C.pool_bn_bwd_reduce(dout, idx, y, stats)
+        dgamma, dbeta = sums[1] * stats[1], sums[0]
+        dy = C.pool_bn_bwd_apply(dout, idx, y, stats, gamma, sums, ctx.training)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            sink = _grad_sink(weight)
+            if sink is not None:
+                C.stem_wgrad(dy, xsp, list(weight.shape), deterministic(), sink)
+                weight._pdt_flat.mark_ready([weight])
+            else:
+                dw = C.stem_wgrad(dy, xsp, list(weight.shape), deterministic()).to(weight.dtype)
+        ctx.weight = None
+        return (None, dw, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, None, None, None,
+                None, None, None)
+
+
+_STEM_POOL = os.environ.get("PDT_STEM_POOL", "1") != "0"  # debugging switch (default on)
+
+
+def _stem_fast(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    return (x.is_cuda and not x.requires_grad and x.dim() == 4 and x.shape[1] <= 4
+            and conv.stride == (2, 2) and conv.kernel_size[0] == conv.kernel_size[1]
+            and conv.bias is None)
+
+
+def stem_conv_bn_pool(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d,
+                      pool: nn.Module) -> torch.Tensor:
+    """maxpool3x3s2(relu(BN(conv7x7/s2(image)))) -> NHWC bf16.  One fused BN/ReLU/pool pass on the
+    device fast path; otherwise the unfused stem followed by the max pool."""
+    std_pool = (isinstance(pool, nn.MaxPool2d) and pool.kernel_size in (3, (3, 3))
+                and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1))
+                and pool.dilation in (1, (1, 1)) and not pool.ceil_mode)
+    if _STEM_POOL and std_pool and _stem_fast(x, conv) and conv.out_channels <= 256:
+        training, momentum, eps = _bn_prepare(bn)
+        return _StemConvBNPool.apply(x.float(), conv.weight, bn.weight, bn.bias, bn.running_mean,
+                                     bn.running_var, 2, conv.padding[0], training, momentum, eps)
+    return maxpool3x3s2(stem_conv_bn(x, conv, bn))
+
+
 def stem_conv_bn(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d) -> torch.Tensor:
     """z = relu(BN(conv7x7/s2(image))) -> NHWC bf16, device path for <= 4-channel fp32 images.
     Falls back to image_to_nhwc + conv_bn when the image itself needs a gradient."""
-    if (not x.is_cuda or x.requires_grad or x.dim() != 4 or x.shape[1] > 4 or conv.stride != (2, 2)
-            or conv.kernel_size[0] != conv.kernel_size[1] or conv.bias is not None):
+    if not _stem_fast(x, conv):
         return conv_bn(image_to_nhwc(x), conv, bn, relu=True)
     training, momentum, eps = _bn_prepare(bn)
     return _StemConvBN.apply(x.float(), conv.weight, bn.weight, bn.bias, bn.running_mean,

@@ -195,6 +195,66 @@ def test_maxpool(gpu, native_ext):
     assert (dx.float() - dxr.float()).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("hw", [(17, 16), (112, 112)])
+def test_bn_relu_maxpool_matches_unfused(gpu, native_ext, hw):
+    """Fused stem BN + ReLU + max pool == bn_act_fwd then maxpool_fwd, bit for bit (values and
+    argmax), and its backward (pooled gradient gathered inside the BN passes) matches
+    maxpool_bwd -> bn_act_bwd_reduce/apply (mask mode 2) up to the bf16 rounding of dz."""
+    C = native_ext
+    g = torch.Generator().manual_seed(21)
+    n, (h, w), k = 4, hw, 64
+    y = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
+    gamma = (torch.rand(k, generator=g) + 0.5).to(gpu)
+    beta = torch.randn(k, generator=g).to(gpu)
+    mean, var = ref.bn_batch_stats(y)
+    invstd = torch.rsqrt(var + 1e-5)
+    scale = (gamma * invstd).contiguous()
+    shift = (beta - mean * scale).contiguous()
+    out, idx = C.bn_relu_maxpool(y, scale, shift)
+    z = C.bn_act_fwd(y, scale, shift, None, True)
+    out_r, idx_r = C.maxpool_fwd(z)
+    assert torch.equal(out, out_r) and torch.equal(idx, idx_r)
+    stats = torch.stack([mean, invstd, scale, shift]).contiguous()
+    dpool = torch.randn(out.shape, generator=g).to(torch.bfloat16).to(gpu)
+    dz = C.maxpool_bwd(dpool, idx, h, w)
+    sums_r = C.bn_act_bwd_reduce(dz, dz, y, stats, 2)
+    dy_r, _ = C.bn_act_bwd_apply(dz, dz, y, stats, gamma, sums_r, 2, True, False)
+    sums = C.pool_bn_bwd_reduce(dpool, idx, y, stats)
+    dy = C.pool_bn_bwd_apply(dpool, idx, y, stats, gamma, sums, True)
+    assert torch.allclose(sums, sums_r, rtol=2e-2, atol=0.5)
+    assert _rel_err(dy, dy_r) < 1e-2
+    # in-place parameter-gradient accumulation variant
+    dgs = torch.ones(k, device=gpu)
+    dbs = torch.ones(k, device=gpu)
+    sums2 = C.pool_bn_bwd_reduce(dpool, idx, y, stats, dgs, dbs)
+    assert torch.equal(sums2, sums)
+    assert torch.allclose(dgs, 1 + sums[1] * invstd, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(dbs, 1 + sums[0], rtol=1e-5, atol=1e-5)
+
+
+def test_stem_pool_fused_matches_unfused_model_path(gpu, native_ext, monkeypatch):
+    """ResNet-50 stem through the fused BN/ReLU/pool node vs the unfused node + max pool:
+    same pooled output, same conv1/bn1 gradients (up to dz's bf16 rounding)."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.ops import fused
+    from pytorch_distributed_tutorials_amd.models import build_model
+    torch.manual_seed(3)
+    m = build_model("resnet50", num_classes=10).to(gpu).set_impl("native")
+    m2 = copy.deepcopy(m)
+    x = torch.randn(8, 3, 64, 64, device=gpu)
+    a = ops.stem_conv_bn_pool(x, m.conv1, m.bn1, m.maxpool)
+    monkeypatch.setattr(fused, "_STEM_POOL", False)
+    b = ops.stem_conv_bn_pool(x, m2.conv1, m2.bn1, m2.maxpool)
+    assert torch.equal(a, b)
+    gout = torch.randn(a.shape, device=gpu).to(torch.bfloat16)
+    a.backward(gout)
+    b.backward(gout)
+    for p1, p2 in [(m.conv1.weight, m2.conv1.weight), (m.bn1.weight, m2.bn1.weight), (m.bn1.bias, m2.bn1.bias)]:
+        assert _rel_err(p1.grad, p2.grad) < 2e-2
+    assert torch.equal(m.bn1.running_mean, m2.bn1.running_mean)
+
+
 def test_avgpool(gpu, native_ext):
     C = native_ext
     x = torch.randn(4, 7, 7, 2048, device=gpu).to(torch.bfloat16)
