@@ -601,45 +601,68 @@ void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float
 // The ReLU mask is recomputed from y (mode 2).  Requires K8 <= 32 and 256 % K8 == 0.
 __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 
-__device__ __forceinline__ f8 pool_grad8(const uint4* __restrict__ dp, const uint2* __restrict__ idx,
-                                         int n, int h, int w, int c8, int C8, int Ho, int Wo) {
-  f8 acc;
+// Quad form of the max-pool gradient gather: input pixels (2a+dh, 2b+dw) of quad (n, a, b) are
+// covered only by the pooled windows W00 = (a, b), W01 = (a, b+1), W10 = (a+1, b), W11 = (a+1, b+1),
+// at fixed window positions: (0,0) <- W00@4; (0,1) <- W00@5 + W01@3; (1,0) <- W00@7 + W10@1;
+// (1,1) <- W00@8 + W01@6 + W10@2 + W11@0.  Four (argmax, gradient) loads serve four pixels,
+// branch-free; windows past the pooled edge get argmax 0xff (never matches).  Quads and pooled
+// outputs coincide one to one (Ho = ceil(H/2) for k3/s2/p1).
+struct PoolQuad { f8 g[4]; };  // g[dh*2 + dw]
+
+__device__ __forceinline__ PoolQuad pool_grad_quad(const uint4* __restrict__ dp, const uint2* __restrict__ idx,
+                                                   int n, int a, int b, int c8, int C8, int Ho, int Wo) {
+  uint2 id[4];
+  f8 gw[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc.v[j] = 0.f;
-  const int ho0 = h >> 1, ho1 = min((h + 1) >> 1, Ho - 1);
-  const int wo0 = w >> 1, wo1 = min((w + 1) >> 1, Wo - 1);
-  for (int ho = ho0; ho <= ho1; ++ho) {
-    const int kh = h - (ho * 2 - 1);
-    for (int wo = wo0; wo <= wo1; ++wo) {
-      const uint32_t pos = (uint32_t)(kh * 3 + (w - (wo * 2 - 1)));
+  for (int wi = 0; wi < 4; ++wi) {
+    const int ho = a + (wi >> 1), wo = b + (wi & 1);
+    if (ho < Ho && wo < Wo) {
       const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C8 + c8;
-      const uint2 id = idx[o];
-      const f8 g = unpack8(dp[o]);
+      id[wi] = idx[o];
+      gw[wi] = unpack8(dp[o]);
+    } else {
+      id[wi] = make_uint2(0xffffffffu, 0xffffffffu);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t b = ((j < 4 ? id.x : id.y) >> (8 * (j & 3))) & 0xffu;
-        if (b == pos) acc.v[j] += g.v[j];
-      }
+      for (int j = 0; j < 8; ++j) gw[wi].v[j] = 0.f;
     }
   }
-  return acc;
+  PoolQuad q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t s[4];
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) s[wi] = ((j < 4 ? id[wi].x : id[wi].y) >> (8 * (j & 3))) & 0xffu;
+    const float g00 = gw[0].v[j], g01 = gw[1].v[j], g10 = gw[2].v[j], g11 = gw[3].v[j];
+    q.g[0].v[j] = s[0] == 4u ? g00 : 0.f;
+    q.g[1].v[j] = (s[0] == 5u ? g00 : 0.f) + (s[1] == 3u ? g01 : 0.f);
+    q.g[2].v[j] = (s[0] == 7u ? g00 : 0.f) + (s[2] == 1u ? g10 : 0.f);
+    q.g[3].v[j] = ((s[0] == 8u ? g00 : 0.f) + (s[1] == 6u ? g01 : 0.f)) +
+                  ((s[2] == 2u ? g10 : 0.f) + (s[3] == 0u ? g11 : 0.f));
+  }
+  return q;
+}
+
+// (n, a, b) of quad / pooled-output index qd (32-bit math; the host bounds the sizes)
+__device__ __forceinline__ void quad_coords(uint32_t qd, int Ho, int Wo, int& n, int& a, int& b) {
+  const uint32_t q2 = qd / (uint32_t)Wo;
+  b = (int)(qd - q2 * (uint32_t)Wo);
+  const uint32_t nn = q2 / (uint32_t)Ho;
+  a = (int)(q2 - nn * (uint32_t)Ho);
+  n = (int)nn;
 }
 
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __restrict__ y,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
                                                               uint4* __restrict__ out,
-                                                              uint2* __restrict__ idx, int N, int H,
-                                                              int W, int C8, int Ho, int Wo) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)N * Ho * Wo * C8;
+                                                              uint2* __restrict__ idx, uint32_t total,
+                                                              int H, int W, int lc8, int Ho, int Wo) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
-  const int c8 = (int)(t % C8);
-  const int64_t p = t / C8;
-  const int wo = (int)(p % Wo);
-  const int64_t q = p / Wo;
-  const int ho = (int)(q % Ho);
-  const int n = (int)(q / Ho);
+  const int C8 = 1 << lc8;
+  const int c8 = (int)(t & (uint32_t)(C8 - 1));
+  int n, ho, wo;
+  quad_coords(t >> lc8, Ho, Wo, n, ho, wo);
   float sc[8], sh[8];
   load8(scale + c8 * 8, sc);
   load8(shift + c8 * 8, sh);
@@ -647,9 +670,11 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
   uint32_t bi[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int h = ho * 2 - 1 + kh;
     if (h < 0 || h >= H) continue;
+#pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int w = wo * 2 - 1 + kw;
       if (w < 0 || w >= W) continue;
@@ -669,12 +694,12 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
                       bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
 }
 
-// stage 1 of the stem BN backward reduction with dz gathered from the pooled gradient
+// stage 1 of the stem BN backward reduction, dz gathered per quad from the pooled gradient
 __global__ void __launch_bounds__(256) pool_bn_bwd_reduce_kernel(const uint4* __restrict__ dp,
                                                                  const uint2* __restrict__ idx,
                                                                  const uint4* __restrict__ y,
                                                                  const float* __restrict__ stats,
-                                                                 int64_t M, int K8, int H, int W,
+                                                                 int NQ, int K8, int H, int W,
                                                                  int Ho, int Wo, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int K = K8 * 8;
@@ -682,27 +707,29 @@ __global__ void __launch_bounds__(256) pool_bn_bwd_reduce_kernel(const uint4* __
   const int c8 = t % K8;
   const int rpi = 256 / K8;
   const int roff = t / K8;
-  const int64_t rows_per_block = (M + gridDim.x - 1) / gridDim.x;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int per_block = (NQ + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int q0 = (int)blockIdx.x * per_block;
+  const int q1 = min(NQ, q0 + per_block);
   float mu[8], sc[8], shf[8];
   load8(stats + c8 * 8, mu);
   load8(stats + 2 * K + c8 * 8, sc);
   load8(stats + 3 * K + c8 * 8, shf);
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int HW = H * W;
-#pragma unroll 2
-  for (int64_t r = r0 + roff; r < r1; r += rpi) {
-    const int n = (int)(r / HW);
-    const int rem = (int)(r - (int64_t)n * HW);
-    const int h = rem / W, w = rem - (rem / W) * W;
-    const f8 d = pool_grad8(dp, idx, n, h, w, c8, K8, Ho, Wo);
-    const f8 yy = unpack8(y[r * K8 + c8]);
+  for (int qd = q0 + roff; qd < q1; qd += rpi) {
+    int n, a, b;
+    quad_coords((uint32_t)qd, Ho, Wo, n, a, b);
+    const PoolQuad pq = pool_grad_quad(dp, idx, n, a, b, c8, K8, Ho, Wo);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float g = relu_grad<2>(d.v[j], 0.f, yy.v[j], sc[j], shf[j]);
-      sg[j] += g;
-      sgx[j] = fmaf(g, yy.v[j] - mu[j], sgx[j]);
+    for (int e = 0; e < 4; ++e) {
+      const int h = 2 * a + (e >> 1), w = 2 * b + (e & 1);
+      if (h >= H || w >= W) continue;
+      const f8 yy = unpack8(y[(((int64_t)n * H + h) * W + w) * K8 + c8]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = relu_grad<2>(pq.g[e].v[j], 0.f, yy.v[j], sc[j], shf[j]);
+        sg[j] += g;
+        sgx[j] = fmaf(g, yy.v[j] - mu[j], sgx[j]);
+      }
     }
   }
   float* my = sh + (size_t)t * 16;
@@ -728,11 +755,11 @@ template <bool TRAIN>
 __global__ void __launch_bounds__(256) pool_bn_bwd_apply_kernel(
     const uint4* __restrict__ dp, const uint2* __restrict__ idx, const uint4* __restrict__ y,
     const float* __restrict__ stats, const float* __restrict__ gamma, const float* __restrict__ sums,
-    int64_t nvec, int K8, int H, int W, int Ho, int Wo, float invM, uint4* __restrict__ dy) {
+    int nvq, int K8, int H, int W, int Ho, int Wo, float invM, uint4* __restrict__ dy) {
   const int K = K8 * 8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int c8 = (int)(tid % K8);
+  const int stride = (int)(gridDim.x * blockDim.x);
+  const int tid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int c8 = tid % K8;
   const int c0 = c8 * 8;
   float k1[8], sgm[8], k2[8], mu[8], sc[8], shf[8];
   {
@@ -751,21 +778,24 @@ __global__ void __launch_bounds__(256) pool_bn_bwd_apply_kernel(
       k2[j] = s1[j] * is[j] * is[j] * invM;
     }
   }
-  const int HW = H * W;
-  for (int64_t v = tid; v < nvec; v += stride) {
-    const int64_t r = v / K8;
-    const int n = (int)(r / HW);
-    const int rem = (int)(r - (int64_t)n * HW);
-    const int h = rem / W, w = rem - (rem / W) * W;
-    const f8 d = pool_grad8(dp, idx, n, h, w, c8, K8, Ho, Wo);
-    const f8 yy = unpack8(y[v]);
-    f8 o;
+  for (int v = tid; v < nvq; v += stride) {
+    int n, a, b;
+    quad_coords((uint32_t)(v / K8), Ho, Wo, n, a, b);
+    const PoolQuad pq = pool_grad_quad(dp, idx, n, a, b, c8, K8, Ho, Wo);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float g = relu_grad<2>(d.v[j], 0.f, yy.v[j], sc[j], shf[j]);
-      o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
+    for (int e = 0; e < 4; ++e) {
+      const int h = 2 * a + (e >> 1), w = 2 * b + (e & 1);
+      if (h >= H || w >= W) continue;
+      const int64_t off = (((int64_t)n * H + h) * W + w) * K8 + c8;
+      const f8 yy = unpack8(y[off]);
+      f8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = relu_grad<2>(pq.g[e].v[j], 0.f, yy.v[j], sc[j], shf[j]);
+        o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
+      }
+      dy[off] = pack8(o);
     }
-    dy[v] = pack8(o);
   }
 }
 
@@ -775,14 +805,21 @@ static void check_pool_bn_channels(int K) {
     throw std::runtime_error("fused BN + max pool: channels must be 8..256 and divide 2048");
 }
 
+static int log2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
 void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* shift, uint16_t* out,
                             uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
   check_pool_bn_channels(C);
   const int C8 = C / 8;
   const int64_t total = (int64_t)N * Ho * Wo * C8;
+  if ((int64_t)N * H * W * C8 >= (int64_t)1 << 31) throw std::runtime_error("bn_relu_maxpool: tensor too large");
   hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const uint4*>(y), scale, shift, reinterpret_cast<uint4*>(out),
-                     reinterpret_cast<uint2*>(idx), N, H, W, C8, Ho, Wo);
+                     reinterpret_cast<uint2*>(idx), (uint32_t)total, H, W, log2_exact(C8), Ho, Wo);
 }
 
 size_t pool_bn_bwd_ws_floats(int64_t M, int K) { return bn_bwd_ws_floats(M, K); }
@@ -793,10 +830,12 @@ void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const 
   check_pool_bn_channels(K);
   const int K8 = K / 8;
   const int64_t M = (int64_t)N * H * W;
-  const int nb = red_blocks(M, K);
+  if (M * K8 >= (int64_t)1 << 31) throw std::runtime_error("pool_bn_bwd_reduce: tensor too large");
+  const int NQ = N * Ho * Wo;
+  const int nb = std::min(red_blocks(M, K), std::max(1, NQ / 8));  // <= bn_bwd_ws_floats(M, K) rows
   hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 256 * 16 * sizeof(float), st,
                      reinterpret_cast<const uint4*>(dpool), reinterpret_cast<const uint2*>(idx),
-                     reinterpret_cast<const uint4*>(y), stats, M, K8, H, W, Ho, Wo, ws);
+                     reinterpret_cast<const uint4*>(y), stats, NQ, K8, H, W, Ho, Wo, ws);
   hipLaunchKernelGGL(bn_bwd_reduce_stage2<8>, dim3(ceil_div(K, 8)), dim3(256), 0, st, ws, nb, K, sums,
                      stats + K, dgamma, dbeta);
 }
@@ -807,18 +846,19 @@ void launch_pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* idx, const u
   check_pool_bn_channels(K);
   const int K8 = K / 8;
   const int64_t M = (int64_t)N * H * W;
-  const int64_t nvec = M * K8;
-  dim3 g(ew_blocks(nvec)), b(256);
+  if (M * K8 >= (int64_t)1 << 31) throw std::runtime_error("pool_bn_bwd_apply: tensor too large");
+  const int nvq = N * Ho * Wo * K8;
+  dim3 g(ew_blocks(nvq)), b(256);  // ew_blocks * 256 is a multiple of K8 (256 % K8 == 0)
   const float invM = 1.f / (float)M;
   auto DP = reinterpret_cast<const uint4*>(dpool);
   auto ID = reinterpret_cast<const uint2*>(idx);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto DY = reinterpret_cast<uint4*>(dy);
   if (training)
-    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<true>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvec,
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<true>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvq,
                        K8, H, W, Ho, Wo, invM, DY);
   else
-    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<false>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvec,
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<false>, g, b, 0, st, DP, ID, Y, stats, gamma, sums, nvq,
                        K8, H, W, Ho, Wo, invM, DY);
 }
 

@@ -1,0 +1,9 @@
+#!/bin/bash
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R"; export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=$R/gpurun_out; mkdir -p $O
+step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc" | tee -a $O/status.txt; return $rc; }
+step pytest_s3f timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -v -x --timeout 120 --timeout-method thread -k "pool or stem or resnet18" || exit 1
+step bench_s3f timeout -k 10 200 python bench.py --steps 30 --warmup 5 || exit 1
+cd /tmp && export TMPDIR=/tmp
+step prof_s3f timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s3f -o run -- python3 $R/bench.py --steps 5 --warmup 3
