@@ -215,7 +215,9 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   const int m0 = tmi * BM, n0 = tni * BN;
 
   const int t = threadIdx.x;
-  const int lane = t & 63, wid = t >> 6;
+  // wave id through readfirstlane: uniform for the compiler, so every LDS-DMA destination
+  // (tile base + wave slot) is scalar math + one m0 write, no VGPR add + readfirstlane per load
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane >> 3, lj = lane & 7;
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
@@ -252,30 +254,65 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     b_row[i] = n < P.Nout ? n * P.Kg : -1;
   }
 
-  const int cb = P.CA / KE;  // 128-byte channel blocks per tap (C64 path)
-  const int nk = C64 ? P.ntaps * cb : (P.Kg + KE - 1) / KE;
+  const int nk = C64 ? P.ntaps * (P.CA / KE) : (P.Kg + KE - 1) / KE;
+
+  // C64 path: per A row, bit t of a_inv = tap t (= ti*tns + tj) reads outside the image.  Built
+  // once from the separable row / column validity; a K-step then turns it into a 0 / all-ones
+  // poison with one bit-field extract and ORs it into the offset (all-ones >= num_records: the
+  // buffer load returns 0) -- 3 VALU per row instead of two adds, two compares and a select.
+  // Closed form, branch-free: along one axis the valid taps t (base + step*t in [0, extent),
+  // step = +-1) form one interval [lo, hi); its bit run is (1<<hi) - (1<<lo).  The 2-D mask is
+  // the column run replicated at the valid tap rows: wm * sum_{ti valid} 2^(ti*tns).
+  uint32_t a_inv[A_PW];
+  if constexpr (C64) {
+    const int nr = P.tnr, ns = P.tns;
+    const uint32_t rep1 = 1u << ns, rep2 = 1u << (2 * ns);  // tap rows 1, 2 (tnr <= 3 fast path)
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) {
+      const int hb = a_h0[i] + P.dr0, wb = a_w0[i] + P.ds0;
+      const int hlo = P.dstep > 0 ? max(0, -hb) : max(0, hb - P.HA + 1);
+      const int hhi = P.dstep > 0 ? min(nr, P.HA - hb) : min(nr, hb + 1);
+      const int wlo = P.dstep > 0 ? max(0, -wb) : max(0, wb - P.WA + 1);
+      const int whi = P.dstep > 0 ? min(ns, P.WA - wb) : min(ns, wb + 1);
+      const uint32_t hm = hhi > hlo ? (1u << (hhi & 31)) - (1u << (hlo & 31)) : 0u;
+      const uint32_t wm = whi > wlo ? (1u << (whi & 31)) - (1u << (wlo & 31)) : 0u;
+      uint32_t spread;
+      if (nr <= 3) {
+        spread = (hm & 1u) | ((hm & 2u) ? rep1 : 0u) | ((hm & 4u) ? rep2 : 0u);
+      } else {
+        spread = 0u;
+        for (int ti = 0; ti < nr; ++ti) spread |= ((hm >> ti) & 1u) << (ti * ns);
+      }
+      a_inv[i] = ~(wm * spread);
+    }
+  }
+  // K-step -> (tap row ti, tap column tj, channel block chb) advanced incrementally (issue() is
+  // called for consecutive K-steps): no scalar divisions in the loop
+  int k_ti = 0, k_tj = 0, k_chb = 0;
 
   auto issue = [&](int kt, int buf) {
     char* As = smem + buf * (BM + BN) * 128;
     char* Bs = As + BM * 128;
     if constexpr (C64) {
-      const int tap = kt / cb;
-      const int chb = (kt - tap * cb) * KE;
-      const int ti = tap / P.tns, tj = tap - ti * P.tns;
-      const int dr = P.dr0 + ti * P.dstep, ds = P.ds0 + tj * P.dstep;
-      const int tbo = ((P.tr0 + ti * P.tstep) * P.S + (P.ts0 + tj * P.tstep)) * P.CA + chb;
-      const int tdelta = ((dr * P.WA + ds) * P.CA + chb) * EB;
+      const int tap = k_ti * P.tns + k_tj;
+      const int dr = P.dr0 + k_ti * P.dstep, ds = P.ds0 + k_tj * P.dstep;
+      const int tbo = ((P.tr0 + k_ti * P.tstep) * P.S + (P.ts0 + k_tj * P.tstep)) * P.CA + k_chb;
+      const int tdelta = ((dr * P.WA + ds) * P.CA + k_chb) * EB;
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
-        const int h = a_h0[i] + dr, w = a_w0[i] + ds;
-        const bool ok = (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
-        const uint32_t off = ok ? (uint32_t)(a_base[i] + tdelta) : OOB;
+        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[i], (unsigned)tap, 1u);
+        const uint32_t off = (uint32_t)(a_base[i] + tdelta) | poison;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
       }
 #pragma unroll
       for (int i = 0; i < B_PW; ++i) {
         uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * EB + b_c[i] * 16) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
+      }
+      k_chb += KE;
+      if (k_chb == P.CA) {
+        k_chb = 0;
+        if (++k_tj == P.tns) { k_tj = 0; ++k_ti; }
       }
     } else {
 #pragma unroll
@@ -607,6 +644,8 @@ struct TnArgs {
   int steps_per_split, nsteps;
   int accumulate;      // single-split direct store: out += acc instead of out = acc
   int staged;          // epilogue through the LDS row image (256-B segments); 0 = direct (A/B knob)
+  int Ho;
+  int adv_r, adv_qh, adv_qn;  // 64 rows = (adv_qn images, adv_qh output rows, adv_r columns)
 };
 
 // LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
@@ -687,7 +726,10 @@ struct TnCfg {
 template <int BMG>
 constexpr int tn_threads() { return BMG == 256 ? 512 : 256; }  // == TnCfg<BMG, ...>::NT
 
-template <int BMG, int BNG, int STAGES, bool ATOMIC>
+// PW: pointwise conv (1x1, stride 1, no padding): the x row of reduction index m IS pixel m, so a
+// B offset is m*C*2 + channel bytes -- no pixel decomposition, no bounds test (rows past the end
+// fall outside the buffer and read 0).
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW>
 __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
   using CFG = TnCfg<BMG, BNG, STAGES>;
   static_assert(CFG::NT == tn_threads<BMG>(), "launch bounds");
@@ -706,39 +748,52 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
   const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
 
   const int t = threadIdx.x;
-  const int lane = t & 63, wid = t >> 6;
+  // uniform wave id (readfirstlane): LDS-DMA destinations become scalar math + one m0 write
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
 
   // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel).
-  // Everything per lane is precomputed; the per-step work is branch-free (selects, no exec
-  // masking): A offset = uniform step base + lane constant, B = one pixel decomposition.
-  int arow[A_PW], a_lane[A_PW];
-  bool a_ok[A_PW];
+  // Everything per lane is precomputed.  Out-of-range columns carry a 2^31 poison in their lane
+  // offset and rows past Mred lie past the end of the buffer, so both read 0 through the buffer
+  // range check: an A load is one add.
+  int a_lane[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
-    arow[i] = (wid * A_PW + i) * CFG::A_RPI + lane / CFG::A_LPR;
+    const int arow = (wid * A_PW + i) * CFG::A_RPI + lane / CFG::A_LPR;
     const int slot = lane % CFG::A_LPR;
-    const int chk = (swz_img<CFG::A_ROWB>(arow[i], slot) - arow[i] * CFG::A_ROWB) >> 4;  // involution
+    const int chk = (swz_img<CFG::A_ROWB>(arow, slot) - arow * CFG::A_ROWB) >> 4;  // involution
     const int acol = k0 + chk * 8;
-    a_ok[i] = acol < P.Kout;
-    a_lane[i] = (arow[i] * P.Kout + acol) * 2;
+    a_lane[i] = acol < P.Kout ? (arow * P.Kout + acol) * 2 : (int)OOB;
   }
   int brow[B_PW], b_dh[B_PW], b_dw[B_PW], b_chb[B_PW];
-  bool b_ok[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     brow[i] = (wid * B_PW + i) * 4 + (lane >> 4);
     const int chk = (swz256(brow[i], lane & 15) - brow[i] * 256) >> 4;
     const int col = c0 + chk * 8;
-    b_ok[i] = col < P.Ncols;
     const int tap = col / P.C;
-    b_chb[i] = (col - tap * P.C) * 2;
+    b_chb[i] = col < P.Ncols ? (col - tap * P.C) * 2 : (int)OOB;
     const int r = tap / P.S;
     b_dh[i] = r - P.pad;
     b_dw[i] = (tap - r * P.S) - P.pad;
   }
   const int WC2 = P.W * P.C * 2, HWC2 = P.H * WC2, C2 = P.C * 2;
+  // general path: (n, ho, wo) of each B row, decomposed once and then advanced by 64 reduction
+  // rows per K-step with two conditional carries (issue() runs for consecutive steps) -- no
+  // quarter-rate multiply-high divisions in the loop.  Rows past Mred continue into n >= N and
+  // land past the buffer end.
+  uint32_t b_n[B_PW], b_ho[B_PW], b_wo[B_PW];
+  if constexpr (!PW) {
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const uint32_t m = (uint32_t)(s_begin * 64 + brow[i]);
+      b_n[i] = fdiv(m, P.div_hw);
+      const uint32_t rem = m - b_n[i] * (uint32_t)P.HoWo;
+      b_ho[i] = fdiv(rem, P.div_w);
+      b_wo[i] = rem - b_ho[i] * (uint32_t)P.Wo;
+    }
+  }
 
   auto issue = [&](int step, int buf) {
     char* As = smem + buf * CFG::STAGE;
@@ -746,21 +801,31 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
     const int mb = step * 64;
     const int abase = mb * P.Kout * 2;
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) {
-      const bool ok = a_ok[i] && (mb + arow[i]) < P.Mred;
-      glds16(rdy, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(abase + a_lane[i]) : OOB);
-    }
+    for (int i = 0; i < A_PW; ++i)
+      glds16(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
-      const int m = mb + brow[i];
-      const uint32_t n = fdiv((uint32_t)m, P.div_hw);
-      const uint32_t rem = (uint32_t)m - n * (uint32_t)P.HoWo;
-      const uint32_t ho = fdiv(rem, P.div_w);
-      const uint32_t wo = rem - ho * (uint32_t)P.Wo;
-      const int h = (int)ho * P.stride + b_dh[i], w = (int)wo * P.stride_w + b_dw[i];
-      const bool ok = b_ok[i] && m < P.Mred && (unsigned)h < (unsigned)P.H && (unsigned)w < (unsigned)P.W;
-      const int off = (int)n * HWC2 + h * WC2 + w * C2 + b_chb[i];
-      glds16(rx, Bs + (wid * B_PW + i) * 1024, ok ? (uint32_t)off : OOB);
+      uint32_t off;
+      if constexpr (PW) {
+        off = (uint32_t)((mb + brow[i]) * C2 + b_chb[i]);
+      } else {
+        // 24-bit multiplies (full rate; every factor < 2^24, products < 2^32), computed
+        // unconditionally and selected: no predicated quarter-rate v_mul_lo_u32 blocks
+        const uint32_t h = __umul24(b_ho[i], (uint32_t)P.stride) + (uint32_t)b_dh[i];
+        const uint32_t w = __umul24(b_wo[i], (uint32_t)P.stride_w) + (uint32_t)b_dw[i];
+        const bool ok = h < (uint32_t)P.H && w < (uint32_t)P.W;
+        const uint32_t o = __umul24(b_n[i], (uint32_t)HWC2) + __umul24(h, (uint32_t)WC2) +
+                           __umul24(w, (uint32_t)C2) + (uint32_t)b_chb[i];
+        off = ok ? o : OOB;
+        uint32_t wo = b_wo[i] + (uint32_t)P.adv_r;
+        const uint32_t c1 = wo >= (uint32_t)P.Wo ? 1u : 0u;
+        b_wo[i] = c1 ? wo - (uint32_t)P.Wo : wo;
+        uint32_t ho = b_ho[i] + (uint32_t)P.adv_qh + c1;
+        const uint32_t c2 = ho >= (uint32_t)P.Ho ? 1u : 0u;
+        b_ho[i] = c2 ? ho - (uint32_t)P.Ho : ho;
+        b_n[i] += (uint32_t)P.adv_qn + c2;
+      }
+      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
     }
   };
 
@@ -1028,7 +1093,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.tnr = s.R; a.tns = s.S; a.ntaps = s.R * s.S;
   a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
-  bool c64 = (s.C % 64) == 0;
+  bool c64 = (s.C % 64) == 0 && s.R * s.S <= 32;  // C64 loader: tap validity bitmask per row
   if (part) {
     if (c64) dispatch_nt<true, EPI_STATS>(a, st, nullptr);
     else dispatch_nt<false, EPI_STATS>(a, st, nullptr);
@@ -1057,7 +1122,7 @@ void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale
   a.tnr = s.R; a.tns = s.S; a.ntaps = s.R * s.S;
   a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
-  const bool c128 = (s.C % 128) == 0;
+  const bool c128 = (s.C % 128) == 0 && s.R * s.S <= 32;
   if (part) {
     if (c128) dispatch_nt<true, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
     else dispatch_nt<false, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
@@ -1117,6 +1182,7 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       a.tnr = r0 < s.R ? (s.R - r0 + str - 1) / str : 0;
       a.tns = s0 < s.S ? (s.S - s0 + str - 1) / str : 0;
       a.ntaps = a.tnr * a.tns;  // 0 -> kernel writes zeros for this class
+      if (a.ntaps > 32) throw std::runtime_error("conv_dgrad: more than 32 taps per parity class");
       a.tr0 = r0; a.ts0 = s0; a.tstep = str;
       a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;
       if (bn != nullptr) {
@@ -1204,10 +1270,10 @@ size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
   return (size_t)p.splits * s.K * s.R * s.S * s.C;
 }
 
-template <int BMG, int BNG, int STAGES, bool ATOMIC>
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW = false>
 static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
   using CFG = TnCfg<BMG, BNG, STAGES>;
-  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC>;
+  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC, PW>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -1245,7 +1311,16 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
-  if (p.bmg == 256) {
+  a.Ho = s.Ho;
+  a.adv_r = 64 % s.Wo;
+  a.adv_qh = (64 / s.Wo) % s.Ho;
+  a.adv_qn = (64 / s.Wo) / s.Ho;
+  const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 &&
+                  s.H == s.Ho && s.W == s.Wo;
+  if (pw && !deep && p.bmg != 256) {
+    if (p.bmg == 64) { if (atomic) run_tn<64, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false, true>(a, p.tiles, p.splits, st); }
+    else { if (atomic) run_tn<128, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 2, false, true>(a, p.tiles, p.splits, st); }
+  } else if (p.bmg == 256) {
     if (atomic) run_tn<256, 128, 2, true>(a, p.tiles, p.splits, st);
     else run_tn<256, 128, 2, false>(a, p.tiles, p.splits, st);
   } else if (p.bmg == 64) {

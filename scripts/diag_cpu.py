@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""CPU-side issue time of the training step (is the host keeping ahead of the GPU?).
+
+Times forward / backward / optimizer issue per step with wall clocks and NO device sync
+inside the loop (launches are asynchronous, so these are host costs as long as the launch
+queue does not fill), then the synchronized step time for comparison.
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_tutorials_amd import ops  # noqa: E402
+from pytorch_distributed_tutorials_amd.models import build_model  # noqa: E402
+from pytorch_distributed_tutorials_amd.optim import SGD  # noqa: E402
+from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel  # noqa: E402
+
+
+def main():
+    arch = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=1000, impl="native").to(dev)
+    model.set_impl("native")
+    ddp = DistributedDataParallel(model)
+    opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+    crit = ops.CrossEntropyLoss()
+    x = torch.randn(256, 3, 224, 224, device=dev)
+    y = torch.randint(0, 1000, (256,), device=dev)
+    for _ in range(5):
+        opt.zero_grad(); crit(ddp(x), y).backward(); opt.step()
+    torch.cuda.synchronize()
+    tf = tb = to = 0.0
+    n = 20
+    t0 = time.perf_counter()
+    for _ in range(n):
+        a = time.perf_counter()
+        opt.zero_grad()
+        loss = crit(ddp(x), y)
+        b = time.perf_counter()
+        loss.backward()
+        c = time.perf_counter()
+        opt.step()
+        d = time.perf_counter()
+        tf += b - a; tb += c - b; to += d - c
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"host issue per step: fwd {1e3*tf/n:.2f} ms  bwd {1e3*tb/n:.2f} ms  opt {1e3*to/n:.2f} ms  "
+          f"total {1e3*(t1-t0)/n:.2f} ms; wall incl. drain {1e3*(t2-t0)/n:.2f} ms/step", flush=True)
+
+
+if __name__ == "__main__":
+    main()
