@@ -123,6 +123,7 @@ struct NtArgs {
   // A-coordinate offset (dr0 + i*dstep, ds0 + j*dstep).  Closed form -> pure scalar math in the
   // K loop (a per-tap table in kernel args would be read with vector loads every K-step).
   int ntaps, tnr, tns, tr0, ts0, tstep, dr0, ds0, dstep;
+  int c8, c8_rows, c8_step;  // generic loader, 8-channel source with S | 8: rows / bytes per K-step
   // EPI_BNB (dgrad): BN-backward of the unit that produced this conv's input, fused into the
   // epilogue.  out = g = dx * relu'(unit) and per-(wave rows, channel) partials of
   // (sum g, sum g*(y - mean)) go to bn_part[bn_group0 + wave_row_group][2][Nout].
@@ -286,6 +287,20 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       a_inv[i] = ~(wm * spread);
     }
   }
+  // c8 loader (non-C64, 8-channel source): per row the first source row of its chunk's tap and
+  // the byte offset of that tap (or OOB when the tap column falls outside the image)
+  int a_c8h[A_PW], a_c8o[A_PW];
+  if constexpr (!C64) {
+    if (P.c8) {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) {
+        const int r0 = a_c[i] / P.S, s0 = a_c[i] - r0 * P.S;
+        const int w = a_w0[i] + s0;
+        a_c8h[i] = a_h0[i] + r0;
+        a_c8o[i] = (unsigned)w < (unsigned)P.WA ? ((a_pix[i] + a_c8h[i] * P.WA + w) * 8 * EB) : (int)OOB;
+      }
+    }
+  }
   // K-step -> (tap row ti, tap column tj, channel block chb) advanced incrementally (issue() is
   // called for consecutive K-steps): no scalar divisions in the loop
   int k_ti = 0, k_tj = 0, k_chb = 0;
@@ -313,6 +328,22 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
       if (k_chb == P.CA) {
         k_chb = 0;
         if (++k_tj == P.tns) { k_tj = 0; ++k_ti; }
+      }
+    } else if (P.c8) {
+      // 8-channel source (the stem's super-pixel image): each 16-B chunk of a K-step is one
+      // whole tap, tap = kt*8 + chunk, and the filter width divides 8, so a K-step advances
+      // the source row by 8/S filter rows: offset = lane constant + kt * row step
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) {
+        const int h = a_c8h[i] + kt * P.c8_rows;
+        const bool ok = (unsigned)h < (unsigned)P.HA && a_c[i] < P.ntaps - kt * 8;
+        glds16(ra, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(a_c8o[i] + kt * P.c8_step) : OOB);
+      }
+#pragma unroll
+      for (int i = 0; i < B_PW; ++i) {
+        const int kk = kt * KE + b_c[i] * CE;
+        uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * EB) : OOB;
+        glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     } else {
 #pragma unroll
@@ -1094,6 +1125,11 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   bool c64 = (s.C % 64) == 0 && s.R * s.S <= 32;  // C64 loader: tap validity bitmask per row
+  if (!c64 && s.C == 8 && 8 % s.S == 0) {
+    a.c8 = 1;
+    a.c8_rows = 8 / s.S;
+    a.c8_step = a.c8_rows * s.W * 8 * 2;
+  }
   if (part) {
     if (c64) dispatch_nt<true, EPI_STATS>(a, st, nullptr);
     else dispatch_nt<false, EPI_STATS>(a, st, nullptr);
