@@ -20,15 +20,17 @@ from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel  
 
 def main():
     arch = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
+    image = int(sys.argv[2]) if len(sys.argv) > 2 else 224
+    classes = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = build_model(arch, num_classes=1000, impl="native").to(dev)
+    model = build_model(arch, num_classes=classes, impl="native").to(dev)
     model.set_impl("native")
     ddp = DistributedDataParallel(model)
     opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
     crit = ops.CrossEntropyLoss()
-    x = torch.randn(256, 3, 224, 224, device=dev)
-    y = torch.randint(0, 1000, (256,), device=dev)
+    x = torch.randn(256, 3, image, image, device=dev)
+    y = torch.randint(0, classes, (256,), device=dev)
     for _ in range(5):
         opt.zero_grad(); crit(ddp(x), y).backward(); opt.step()
     torch.cuda.synchronize()
