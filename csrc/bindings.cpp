@@ -148,7 +148,7 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& wk, int64_t s
   float* pp = nullptr;
   int M = s.N * s.Ho * s.Wo;
   if (stats) {
-    int grows = pdt::conv_fwd_group_rows(M, s.K);
+    int grows = pdt::conv_nt_group_rows(M, s.K, s.R * s.S * s.C * 2);
     int ng = (M + grows - 1) / grows;
     part = at::empty({ng, 2, s.K}, x.options().dtype(at::kFloat));
     pp = part.data_ptr<float>();
@@ -225,7 +225,7 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
     TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
     ap = cbf(*addend);
   }
-  const int G = pdt::conv_dgrad_bn_groups(s);
+  const int G = pdt::conv_dgrad_bn_groups(s, (int)dy_like.element_size());
   auto fopt = y.options().dtype(at::kFloat);
   auto part = at::empty({(int64_t)G * 2 * s.C}, fopt);
   auto ws = at::empty({(int64_t)pdt::bn_bwd_part_ws_floats(G, s.C)}, fopt);
@@ -385,7 +385,7 @@ std::tuple<Tensor, Tensor, Tensor> stem_conv_fwd(const Tensor& x, const Tensor& 
   float* pp = nullptr;
   if (stats) {
     const int M = N * Ho * Wo;
-    const int grows = pdt::conv_fwd_group_rows(M, K);
+    const int grows = pdt::conv_nt_group_rows(M, K, R * Sp * 8 * 2);
     part = at::empty({(M + grows - 1) / grows, 2, K}, x.options());
     pp = part.data_ptr<float>();
   }
@@ -435,8 +435,16 @@ Tensor bn_finalize(const Tensor& part, int64_t count, const Tensor& rm, const Te
   check_cuda(part, "part");
   c10::hip::HIPGuard g(part.get_device());
   int ng = part.size(0), K = part.size(2);
-  int grows = pdt::conv_fwd_group_rows((int)count, K);
-  TORCH_CHECK((count + grows - 1) / grows == ng, "bn_finalize: partial layout mismatch");
+  // the producing conv's row group is its NT tile's BM (64, 128 or 256; conv_nt_group_rows): the
+  // only one of those giving ng groups over `count` rows; a single group covers every row
+  int grows = 0;
+  if (ng == 1) {
+    grows = (int)count;
+  } else {
+    for (int g : {64, 128, 256})
+      if ((count + g - 1) / g == ng) { grows = g; break; }
+  }
+  TORCH_CHECK(grows > 0, "bn_finalize: partial layout mismatch");
   int P = pdt::bn_finalize_partitions(ng);
   auto out = at::empty({4 * K + 3 * K * P}, part.options());
   TORCH_CHECK(gamma.scalar_type() == at::kFloat && rm.scalar_type() == at::kFloat, "BN params must be fp32");
@@ -881,7 +889,7 @@ std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const
   float* pp = nullptr;
   int M = s.N * s.Ho * s.Wo;
   if (stats) {
-    int grows = pdt::conv_fwd_group_rows(M, s.K);
+    int grows = pdt::conv_nt_group_rows(M, s.K, s.R * s.S * s.C);
     part = at::empty({(M + grows - 1) / grows, 2, s.K}, x.options().dtype(at::kFloat));
     pp = part.data_ptr<float>();
   }
@@ -983,7 +991,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("mfma_f8_probe", checked("mfma_f8_probe", &mfma_f8_probe), py::arg("a"), py::arg("b"),
         py::arg("fmt_a") = 0, py::arg("fmt_b") = 0, py::arg("scale_a") = 127, py::arg("scale_b") = 127,
         py::arg("use_scale") = true);
-  m.def("conv_fwd_group_rows", &pdt::conv_fwd_group_rows);
+  m.def("conv_nt_group_rows", &pdt::conv_nt_group_rows, py::arg("M"), py::arg("Nout"), py::arg("kg_bytes"));
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });
 

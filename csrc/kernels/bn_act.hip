@@ -42,24 +42,28 @@ static bool bn_lastblock() {
   return v == 1;
 }
 
-// Last-arriver handshake (agent-scope release/acquire, MI355X_MICROARCH Guideline 16 pattern):
-// every block publishes its partial with plain stores; the block that completes tile `tile` last
-// gets true and may then read all partials of that tile with plain loads.
+// Last-arriver handshake without fences (MI355X_MICROARCH "Hand-offs measured with sc1 loads",
+// first row): every block publishes its stage-1 partial with write-through stores (st_wt: agent-
+// scope relaxed = global_store sc1), every storing wave drains them (vmcnt 0), a barrier, then ONE
+// lane adds to the tile's unsharded counter; the block whose add returns nblocks-1 is the last one
+// and reads the partials with L1-bypassing loads (ld_wt: global_load sc1).  No agent release
+// (buffer_wbl2, >= 1.7 us) in every block and no acquire (buffer_inv, ~1.7 us) in the last one:
+// both sat on the critical path of ~100 tiny reductions per ResNet-50 step.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ bool last_block_of_tile(int tile, unsigned int nblocks) {
   __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its st_wt stores landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned int prev = __hip_atomic_fetch_add(&g_tile_counters[tile], 1u, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
     const bool last = prev == nblocks - 1;
-    if (last) {
-      __hip_atomic_store(&g_tile_counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(&g_tile_counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last ? 1 : 0;
   }
   __syncthreads();
@@ -103,7 +107,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   if (ty == 0 && k < K) {
     for (int r = 1; r < FIN_ROWS; ++r) { S += sS[r][tx]; A += sA[r][tx]; B += sB[r][tx]; }
     float* o = ws + ((int64_t)blockIdx.y * 3) * K;
-    o[k] = S; o[K + k] = A; o[2 * K + k] = B;
+    st_wt(o + k, S); st_wt(o + K + k, A); st_wt(o + 2 * K + k, B);
   }
   if (mode == 1) return;
   if (!last_block_of_tile(blockIdx.x, gridDim.y)) return;
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
 #pragma unroll 8
     for (int p = ty; p < P; p += FIN_ROWS) {
       const float* o = ws + ((int64_t)p * 3) * K;
-      S += o[k]; A += o[K + k]; B += o[2 * K + k];
+      S += ld_wt(o + k); A += ld_wt(o + K + k); B += ld_wt(o + 2 * K + k);
     }
   }
   sS[ty][tx] = S; sA[ty][tx] = A; sB[ty][tx] = B;
@@ -403,8 +407,8 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   if (ty == 0 && k < K) {
     for (int r = 1; r < FIN_ROWS; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
     float* o = ws + (int64_t)blockIdx.y * 2 * K;
-    o[k] = a;
-    o[K + k] = b;
+    st_wt(o + k, a);
+    st_wt(o + K + k, b);
   }
   if (mode == 1) return;
   if (!last_block_of_tile(kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
@@ -414,8 +418,8 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   if (k < K) {
 #pragma unroll 8
     for (int p = ty; p < P; p += FIN_ROWS) {
-      a += ws[(int64_t)p * 2 * K + k];
-      b += ws[(int64_t)p * 2 * K + K + k];
+      a += ld_wt(ws + (int64_t)p * 2 * K + k);
+      b += ld_wt(ws + (int64_t)p * 2 * K + K + k);
     }
   }
   sa[ty][tx] = a;

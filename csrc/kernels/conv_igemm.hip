@@ -17,7 +17,7 @@
 //              classes (one launch each) so no MFMA work is spent on the
 //              structural zeros of the transposed convolution.  The fwd
 //              epilogue also emits BatchNorm partial statistics (sum and M2 per
-//              16*TM-row group per channel) from the fp32 accumulators, so BN
+//              workgroup row tile per channel) from the fp32 accumulators, so BN
 //              never re-reads the conv output to compute its batch stats.
 //   igemm_tn : wgrad.  Both operands have the reduction index (pixels) as the
 //              strided dimension, so tiles are staged [m][col] and fragments are
@@ -125,8 +125,8 @@ struct NtArgs {
   int ntaps, tnr, tns, tr0, ts0, tstep, dr0, ds0, dstep;
   int c8, c8_rows, c8_step;  // generic loader, 8-channel source with S | 8: rows / bytes per K-step
   // EPI_BNB (dgrad): BN-backward of the unit that produced this conv's input, fused into the
-  // epilogue.  out = g = dx * relu'(unit) and per-(wave rows, channel) partials of
-  // (sum g, sum g*(y - mean)) go to bn_part[bn_group0 + wave_row_group][2][Nout].
+  // epilogue.  out = g = dx * relu'(unit) and per-(workgroup row tile, channel) partials of
+  // (sum g, sum g*(y - mean)) go to bn_part[bn_group0 + row_tile][2][Nout].
   const uint16_t* bn_y;   // that unit's pre-BN conv output (same layout as out)
   const uint16_t* bn_z;   // its post-activation output (mask mode 1 only), or for mask mode 3 its
                           // ReLU bitmask: one byte per 8-channel chunk, bit q = (z[c0 + q] > 0)
@@ -453,14 +453,16 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   }
 
   if constexpr (EPI == EPI_STATS) {
-    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels;
-    // the writer converts to M2 about the group mean (cancellation is benign at 64 rows; groups
-    // are combined with Chan's parallel formula in bn_finalize).
-    const int group = tmi * WM + wm;
-    const int valid = min(TM * 16, P.M - wrow0);
-    if (valid > 0) {
+    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels,
+    // converted to M2 about the wave's mean (cancellation is benign at <= 64 rows).  The WM wave
+    // rows of the workgroup are then merged in LDS (Chan: M2 = sum M2_w + sum n_w (mean_w -
+    // mean)^2), so ONE partial per (workgroup row tile, channel) goes out and bn_finalize reads
+    // BM-row groups (4x fewer partials on the 256-row tiles than per-wave groups).
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]: the pipeline buffers are idle now
+    const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
+    {
       const bool full = valid == TM * 16;  // wave-uniform: no per-element masking on full tiles
-      const float inv_valid = 1.f / (float)valid;
+      const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         float s[4], q[4];
@@ -486,15 +488,41 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
           s[e] = v;
           q[e] = fmaxf(v2 - v * v * inv_valid, 0.f);
         }
-        const int col = wcol0 + j * 16 + fq * 4;
-        if (fr == 0 && col < P.Nout) {
-          *reinterpret_cast<float4*>(P.part + ((int64_t)group * 2 + 0) * P.Nout + col) =
-              make_float4(s[0], s[1], s[2], s[3]);
-          *reinterpret_cast<float4*>(P.part + ((int64_t)group * 2 + 1) * P.Nout + col) =
-              make_float4(q[0], q[1], q[2], q[3]);
+        if (fr == 0) {
+          const int cl = wn * TN * 16 + j * 16 + fq * 4;  // column within the workgroup tile
+          *reinterpret_cast<float4*>(red + (wm * 2 + 0) * BN + cl) = make_float4(s[0], s[1], s[2], s[3]);
+          *reinterpret_cast<float4*>(red + (wm * 2 + 1) * BN + cl) = make_float4(q[0], q[1], q[2], q[3]);
         }
       }
     }
+    __syncthreads();
+    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
+      float sw[WM], qw[WM], nw[WM];
+      float S = 0.f, Nr = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        nw[w] = (float)max(0, min(TM * 16, P.M - (m0 + w * TM * 16)));
+        sw[w] = red[(w * 2 + 0) * BN + t];
+        qw[w] = red[(w * 2 + 1) * BN + t];
+        S += sw[w];
+        Nr += nw[w];
+      }
+      const float mean = S / Nr;  // Nr > 0: the tile's first wave row is inside the GEMM
+      float Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        if (nw[w] > 0.f) {
+          const float d = sw[w] / nw[w] - mean;
+          Q += qw[w] + nw[w] * d * d;
+        }
+      }
+      const int col = n0 + t;
+      if (col < P.Nout) {
+        P.part[((int64_t)tmi * 2 + 0) * P.Nout + col] = S;
+        P.part[((int64_t)tmi * 2 + 1) * P.Nout + col] = Q;
+      }
+    }
+    __syncthreads();  // red[] aliases the staging rows written next
   }
 
   // stage the wave's pixels x channels tile as bf16 (8-byte writes), then 16-byte row stores
@@ -649,13 +677,28 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
         bsg[q] += __shfl_xor(bsg[q], o, 64);
         bsq[q] += __shfl_xor(bsq[q], o, 64);
       }
-    const int colw = wcol0 + lane * 8;
-    if (lane < CH_PER_ROW && wrow0 < P.M && colw < P.Nout) {
-      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + wrow0 / (TM * 16)) * 2) * P.Nout + colw;
-      *reinterpret_cast<float4*>(pp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
-      *reinterpret_cast<float4*>(pp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
-      *reinterpret_cast<float4*>(pp + P.Nout) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
-      *reinterpret_cast<float4*>(pp + P.Nout + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
+    // then the WM wave rows of the workgroup are summed in LDS (fixed order): one partial per
+    // (workgroup row tile, channel).  Waves past the GEMM edge hold zeros.
+    __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    if (lane < CH_PER_ROW) {
+      float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
+      *reinterpret_cast<float4*>(rp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
+      *reinterpret_cast<float4*>(rp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
+      *reinterpret_cast<float4*>(rp + BN) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
+      *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
+    }
+    __syncthreads();
+    if (t < BN && n0 + t < P.Nout) {
+      float S = 0.f, Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        S += red[(w * 2) * BN + t];
+        Q += red[(w * 2 + 1) * BN + t];
+      }
+      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + tmi) * 2) * P.Nout + n0 + t;
+      pp[0] = S;
+      pp[P.Nout] = Q;
     }
   }
 }
@@ -1062,41 +1105,47 @@ static int nt_tile_mode() {
   return v;
 }
 
-static bool use_wide_tile(const NtArgs& a, int kg_bytes) {
+static bool use_wide_tile(int M, int Nout, int kg_bytes) {
   const int mode = nt_tile_mode();
-  if (mode == 1 || a.Nout < 256) return false;
+  if (mode == 1 || Nout < 256) return false;
   if (mode == 2) return true;
-  const int64_t blocks = (int64_t)((a.M + 255) / 256) * ((a.Nout + 255) / 256);
+  const int64_t blocks = (int64_t)((M + 255) / 256) * ((Nout + 255) / 256);
   return kg_bytes >= 256 && blocks >= 196;
 }
 
-// tile choice: output channels 64 -> tall tile (more M rows per block); small M -> short tile;
-// big GEMMs -> 256x256
+// Tile choice: output channels 64 -> tall 256x64 tile (more M rows per block); small M -> short
+// 64x128 tile; big GEMMs -> 256x256, else 128x128.  Returns the tile's BM, which is also the row
+// group of the BN partials the STATS / BNB epilogues write (one per workgroup row tile): hosts
+// size those buffers with it, dispatch_nt picks its tile with it -- one definition for both.
+int conv_nt_group_rows(int M, int Nout, int kg_bytes) {
+  if (Nout <= 64) return 256;
+  if (M <= 8192) return 64;
+  return use_wide_tile(M, Nout, kg_bytes) ? 256 : 128;
+}
+
 template <bool C64, int EPI, int OP = OP_BF16>
-static void dispatch_nt(const NtArgs& a, hipStream_t st, int* group_rows) {
-  if (group_rows) *group_rows = (a.Nout > 64 && a.M <= 8192) ? 32 : 64;
+static void dispatch_nt(const NtArgs& a, hipStream_t st) {
+  const int rows = conv_nt_group_rows(a.M, a.Nout, a.Kg * (OP == OP_BF16 ? 2 : 1));
   if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
     if (a.Nout <= 64) run_nt<4, 1, 4, 4, 2, C64, EPI, OP>(a, st);
-    else if (a.M <= 8192) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
-    else if (use_wide_tile(a, a.Kg)) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
+    else if (rows == 64) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
+    else if (rows == 256) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
     else run_nt<2, 2, 4, 4, 2, C64, EPI, OP>(a, st);
     return;
   }
   if (a.Nout <= 64) {
     if (nt_stages(0) == 3) run_nt<4, 1, 4, 4, 3, C64, EPI>(a, st);  // 256 x 64
     else run_nt<4, 1, 4, 4, 2, C64, EPI>(a, st);
-  } else if (a.M <= 8192) {
+  } else if (rows == 64) {
     if (nt_stages(1) == 3) run_nt<2, 2, 2, 4, 3, C64, EPI>(a, st);  // 64 x 128
     else run_nt<2, 2, 2, 4, 2, C64, EPI>(a, st);
-  } else if (use_wide_tile(a, a.Kg * 2)) {
+  } else if (rows == 256) {
     run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);  // 256 x 256
   } else {
     if (nt_stages(2) == 3) run_nt<2, 2, 4, 4, 3, C64, EPI>(a, st);  // 128 x 128
     else run_nt<2, 2, 4, 4, 2, C64, EPI>(a, st);
   }
 }
-
-int conv_fwd_group_rows(int M, int Nout) { return Nout <= 64 ? 64 : (M <= 8192 ? 32 : 64); }
 
 static void fill_common(NtArgs& a, int Mi, int Mj) {
   a.Mij = Mi * Mj;
@@ -1131,11 +1180,11 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
     a.c8_step = a.c8_rows * s.W * 8 * 2;
   }
   if (part) {
-    if (c64) dispatch_nt<true, EPI_STATS>(a, st, nullptr);
-    else dispatch_nt<false, EPI_STATS>(a, st, nullptr);
+    if (c64) dispatch_nt<true, EPI_STATS>(a, st);
+    else dispatch_nt<false, EPI_STATS>(a, st);
   } else {
-    if (c64) dispatch_nt<true, EPI_PLAIN>(a, st, nullptr);
-    else dispatch_nt<false, EPI_PLAIN>(a, st, nullptr);
+    if (c64) dispatch_nt<true, EPI_PLAIN>(a, st);
+    else dispatch_nt<false, EPI_PLAIN>(a, st);
   }
 }
 
@@ -1160,11 +1209,11 @@ void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   const bool c128 = (s.C % 128) == 0 && s.R * s.S <= 32;
   if (part) {
-    if (c128) dispatch_nt<true, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
-    else dispatch_nt<false, EPI_STATS, OP_F8_E4M3>(a, st, nullptr);
+    if (c128) dispatch_nt<true, EPI_STATS, OP_F8_E4M3>(a, st);
+    else dispatch_nt<false, EPI_STATS, OP_F8_E4M3>(a, st);
   } else {
-    if (c128) dispatch_nt<true, EPI_PLAIN, OP_F8_E4M3>(a, st, nullptr);
-    else dispatch_nt<false, EPI_PLAIN, OP_F8_E4M3>(a, st, nullptr);
+    if (c128) dispatch_nt<true, EPI_PLAIN, OP_F8_E4M3>(a, st);
+    else dispatch_nt<false, EPI_PLAIN, OP_F8_E4M3>(a, st);
   }
 }
 
@@ -1175,12 +1224,12 @@ static int dgrad_class_rows(const ConvShape& s, int ph, int pw) {
   return (Mi <= 0 || Mj <= 0) ? 0 : s.N * Mi * Mj;
 }
 
-int conv_dgrad_bn_groups(const ConvShape& s) {
+int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes) {
   int g = 0;
   for (int ph = 0; ph < s.stride; ++ph)
     for (int pw = 0; pw < s.stride; ++pw) {
       const int M = dgrad_class_rows(s, ph, pw);
-      if (M > 0) g += ceil_div(M, conv_fwd_group_rows(M, s.C));
+      if (M > 0) g += ceil_div(M, conv_nt_group_rows(M, s.C, s.R * s.S * s.K * elem_bytes));
     }
   return g;
 }
@@ -1224,10 +1273,10 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       if (bn != nullptr) {
         a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part;
         a.bn_mask = bn->mask; a.bn_group0 = group0;
-        group0 += ceil_div(a.M, conv_fwd_group_rows(a.M, a.Nout));
-        dispatch_nt<true, EPI_BNB, OP>(a, st, nullptr);
+        group0 += ceil_div(a.M, conv_nt_group_rows(a.M, a.Nout, a.Kg * EB));
+        dispatch_nt<true, EPI_BNB, OP>(a, st);
       } else {
-        dispatch_nt<true, EPI_PLAIN, OP>(a, st, nullptr);
+        dispatch_nt<true, EPI_PLAIN, OP>(a, st);
       }
     }
 }

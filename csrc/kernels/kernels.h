@@ -47,8 +47,9 @@ struct ConvShape {
   int sw() const { return stride_w > 0 ? stride_w : stride; }
 };
 // y[N,Ho,Wo,K] = conv(x, w[K][R][S][C]); if part != nullptr also writes per-group
-// BN partials part[ceil(M/G)][2][K] = (sum, M2 about the group mean), G = conv_fwd_group_rows().
-int conv_fwd_group_rows(int M, int Nout);
+// BN partials part[ceil(M/G)][2][K] = (sum, M2 about the group mean), G = conv_nt_group_rows(M, K,
+// R*S*C*elem_bytes) = the BM of the workgroup tile the launch uses (one group per row tile).
+int conv_nt_group_rows(int M, int Nout, int kg_bytes);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
                      const ConvShape& s, hipStream_t st);
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);
@@ -56,7 +57,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
 // Optional fused BatchNorm backward of the unit whose output x was (dx = dL/dx of that unit's
 // activation): the kernel stores g = dx * relu'(.) instead of dx (mask 0: none, 1: z > 0,
 // 2: y*scale + shift > 0) and writes per-row-group partials part[G][2][C] of
-// (sum g, sum g*(y - mean)), G = conv_dgrad_bn_groups(s); reduce them with
+// (sum g, sum g*(y - mean)), G = conv_dgrad_bn_groups(s, bytes per dy element); reduce them with
 // launch_bn_bwd_part_reduce.
 struct BnBwdFuse {
   const uint16_t* y;     // [N,H,W,C] pre-BN output of that unit
@@ -66,7 +67,7 @@ struct BnBwdFuse {
   float* part;           // [G][2][C]
   int mask;
 };
-int conv_dgrad_bn_groups(const ConvShape& s);
+int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes = 2);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
                        const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr);
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
