@@ -12,6 +12,11 @@ does not hand their memory out while the side stream still reads them; gradient
 all-reduces wait for the side stream (``Reducer.set_aux_stream``); and a callback
 at the end of backward joins it into the caller's stream, so the optimizer step
 sees every gradient.  ``PDT_WGRAD_STREAM=0`` turns it off.
+
+One join per backward pass suffices: ``begin`` queues it for the first block of a
+graph task only.  (Handing a block's wgrads over in one batch instead of one per
+wgrad was measured slower: 11.9k vs 12.0k img/s, the wgrads lose their overlap
+with their own block's dgrad chain.)
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ import torch
 
 _enabled = os.environ.get("PDT_WGRAD_STREAM", "1") != "0"
 _streams: Dict[int, torch.cuda.Stream] = {}
+_joined_task = [None]  # graph task whose end-of-backward join is already queued
 
 
 def set_enabled(on: bool) -> None:
@@ -42,12 +48,16 @@ def wgrad_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
 
 def begin(device: torch.device) -> Optional[torch.cuda.Stream]:
     """Called inside a backward that will put work on the side stream: queues the join of the
-    side stream into the caller's stream at the end of this backward pass."""
+    side stream into the caller's stream at the end of this backward pass (once per pass: the
+    graph task id tells passes apart, so an aborted pass cannot suppress the next one's join)."""
     s = wgrad_stream(device)
     if s is None:
         return None
-    cur = torch.cuda.current_stream(device)
-    torch.autograd.Variable._execution_engine.queue_callback(lambda: cur.wait_stream(s))
+    task = (torch._C._current_graph_task_id(), device.index)
+    if task[0] < 0 or _joined_task[0] != task:
+        _joined_task[0] = task
+        cur = torch.cuda.current_stream(device)
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: cur.wait_stream(s))
     return s
 
 
@@ -60,3 +70,4 @@ def launch(side: torch.cuda.Stream, fn, *inputs: torch.Tensor):
     for t in inputs:
         t.record_stream(side)
     return out
+
