@@ -11,6 +11,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <numeric>
 #include <stdexcept>
 
 namespace pdt {
@@ -180,6 +181,12 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 }
 
 // ------------------------------------------------------------------- forward
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 template <bool RES, bool RELU, bool MASK = false>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict__ y,
                                                          const float* __restrict__ scale,
@@ -187,16 +194,16 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
                                                          const uint4* __restrict__ res,
                                                          uint4* __restrict__ z, int64_t nvec,
                                                          int K8, uint8_t* __restrict__ zmask = nullptr) {
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    int c0 = (int)(v % K8) * 8;
+  // the grid stride is a multiple of K8 (ew_blocks), so a thread's 8-channel group and its
+  // scale/shift are fixed over the loop (no 64-bit modulo and 4 coefficient loads per vector)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(v0 % K8) * 8;
+  float sc[8], sh[8];
+  load8(scale + c0, sc);
+  load8(shift + c0, sh);
+  for (int64_t v = v0; v < nvec; v += stride) {
     f8 a = unpack8(y[v]);
-    float4 s0 = *reinterpret_cast<const float4*>(scale + c0);
-    float4 s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
-    float4 h0 = *reinterpret_cast<const float4*>(shift + c0);
-    float4 h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
-    float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     f8 r;
     if (RES) r = unpack8(res[v]);
 #pragma unroll
@@ -218,9 +225,13 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
   }
 }
 
-static int ew_blocks(int64_t nvec) {
+// grid of an 8-channel-vector elementwise pass: <= 8192 blocks of 256, rounded so that the grid
+// stride (blocks * 256) is a multiple of K8 -- every thread then keeps one channel group
+static int ew_blocks(int64_t nvec, int K8) {
   int64_t b = (nvec + 255) / 256;
-  return (int)(b < 8192 ? b : 8192);
+  b = b < 8192 ? b : 8192;
+  const int64_t q = K8 / std::gcd(K8, 256);
+  return (int)(((b + q - 1) / q) * q);
 }
 
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
@@ -228,7 +239,7 @@ void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift
                        hipStream_t st, uint8_t* zmask) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
-  dim3 g(ew_blocks(nvec)), b(256);
+  dim3 g(ew_blocks(nvec, K8)), b(256);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto R = reinterpret_cast<const uint4*>(res);
   auto Z = reinterpret_cast<uint4*>(z);
@@ -277,12 +288,6 @@ __device__ __forceinline__ float relu_grad(float g, float zv, float yv, float sc
   if (MASK == 1) return zv > 0.f ? g : 0.f;
   if (MASK == 2) return fmaf(yv, sc, sh) > 0.f ? g : 0.f;
   return g;
-}
-
-__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
-  float4 a = *reinterpret_cast<const float4*>(p);
-  float4 b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 // stats = [4][K]: mean, invstd, scale, shift (bn_finalize output)
@@ -535,7 +540,7 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
                              hipStream_t st) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
-  dim3 g(ew_blocks(nvec)), b(256);
+  dim3 g(ew_blocks(nvec, K8)), b(256);
   auto DZ = reinterpret_cast<const uint4*>(dz);
   auto Z = reinterpret_cast<const uint4*>(z);
   auto Y = reinterpret_cast<const uint4*>(y);
@@ -852,7 +857,7 @@ void launch_pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* idx, const u
   const int64_t M = (int64_t)N * H * W;
   if (M * K8 >= (int64_t)1 << 31) throw std::runtime_error("pool_bn_bwd_apply: tensor too large");
   const int nvq = N * Ho * Wo * K8;
-  dim3 g(ew_blocks(nvq)), b(256);  // ew_blocks * 256 is a multiple of K8 (256 % K8 == 0)
+  dim3 g(ew_blocks(nvq, K8)), b(256);  // ew_blocks * 256 is a multiple of K8
   const float invM = 1.f / (float)M;
   auto DP = reinterpret_cast<const uint4*>(dpool);
   auto ID = reinterpret_cast<const uint2*>(idx);

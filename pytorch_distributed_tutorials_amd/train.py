@@ -91,7 +91,63 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--deterministic", action=argparse.BooleanOptionalAction, default=True,
                    help="bitwise-reproducible kernels (reference sets cudnn.deterministic=True); "
                         "--no-deterministic enables atomic split-K weight gradients")
+    p.add_argument("--graph", action="store_true",
+                   help="native impl on a GPU: capture the whole training step (forward, backward with "
+                        "the bucketed all-reduces, SGD) in a HIP graph once and replay it for every "
+                        "full-size batch; the launch-bound ResNet-18/CIFAR step gains the most")
     return p
+
+
+class _GraphStep:
+    """One training step replayed from a HIP graph (``utils.graph.CapturedStep``).
+
+    The first WARMUP full-size batches train eagerly (lazy initialisation, allocator pools,
+    kernel attributes); the next one is copied into static input tensors, captured (capture
+    executes nothing) and replayed, and so is every later full-size batch -- every batch is
+    trained on exactly once.  A batch of another shape (an epoch's last, partial batch) runs
+    eagerly.  The CPU bookkeeping of the step (reducer hooks, BN counters, weight-mirror
+    versions) runs during capture only, which is valid because the ResNet step is static.
+    """
+
+    WARMUP = 3
+
+    def __init__(self, ddp_model, criterion, optimizer):
+        self.ddp_model, self.criterion, self.optimizer = ddp_model, criterion, optimizer
+        self.x = self.y = None
+        self.warm = 0
+        self.side = None
+        self.captured = None
+
+    def eager(self, inputs, labels):
+        self.optimizer.zero_grad()
+        loss = self.criterion(self.ddp_model(inputs), labels)
+        loss.backward()
+        self.optimizer.step()
+        return loss
+
+    def __call__(self, inputs, labels):
+        from .utils.graph import CapturedStep
+        if self.x is not None and (inputs.shape != self.x.shape or labels.shape != self.y.shape):
+            return self.eager(inputs, labels)
+        if self.warm < self.WARMUP:
+            self.warm += 1
+            if self.warm == self.WARMUP:  # the full-size batch shape the graph is captured for
+                self.x, self.y = inputs.clone(), labels.clone()
+            # on a side stream, as torch prescribes for pre-capture warm-up: autograd nodes created
+            # here (AccumulateGrad) must not tie the captured backward to the legacy default stream
+            cur = torch.cuda.current_stream()
+            if self.side is None:
+                self.side = torch.cuda.Stream()
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                loss = self.eager(inputs, labels)
+            cur.wait_stream(self.side)
+            return loss
+        self.x.copy_(inputs)
+        self.y.copy_(labels)
+        if self.captured is None:
+            self.captured = CapturedStep(lambda: self.eager(self.x, self.y), warmup=0)
+        return self.captured()
 
 
 def evaluate(model: nn.Module, device: torch.device, test_loader) -> float:
@@ -126,7 +182,11 @@ def main(argv: Optional[list] = None) -> int:
     if dtype == "fp8":
         if impl != "native" or device.type != "cuda":
             raise SystemExit("--dtype fp8 needs the native impl on a GPU")
+        if args.graph:
+            raise SystemExit("--graph with --dtype fp8: the delayed-scaling slots advance per call")
         ops.set_fp8(True)
+    if args.graph and (impl != "native" or device.type != "cuda"):
+        raise SystemExit("--graph needs the native impl on a GPU")
     autocast = (impl == "torch" and dtype == "bf16")
     if args.trace:
         trace.enable(True)
@@ -167,6 +227,7 @@ def main(argv: Optional[list] = None) -> int:
                                 device=device, seed=args.seed + env.rank)
     test_loader = DeviceLoader(test_set, 128, shuffle=False, augment=False, device=device)
 
+    graph_step = _GraphStep(ddp_model, criterion, optimizer) if args.graph else None
     global_step = 0
     done = False
     for epoch in range(start_epoch, args.num_epochs):
@@ -175,7 +236,11 @@ def main(argv: Optional[list] = None) -> int:
             if watchdog is not None:
                 watchdog.heartbeat("eval")
             with trace.trace_range("eval"):
-                accuracy = evaluate(model=ddp_model, device=device, test_loader=test_loader)
+                # a replayed graph cannot skip its captured buffer broadcast the way an eager
+                # forward after a rank-0-only eval does, so with --graph rank 0
+                # evaluates the wrapped module itself: no collective, same buffers
+                accuracy = evaluate(model=ddp_model.module if graph_step is not None else ddp_model,
+                                    device=device, test_loader=test_loader)
             save_checkpoint(ddp_model, model_filepath, optimizer, epoch)
             print("-" * 75)
             print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
@@ -194,14 +259,19 @@ def main(argv: Optional[list] = None) -> int:
                 watchdog.heartbeat(f"epoch {epoch} step {step}")
             inject(global_step)
             inputs, labels = inputs.to(device), labels.to(device)
-            optimizer.zero_grad()
-            with trace.trace_range("forward"), torch.autocast(device.type, torch.bfloat16, enabled=autocast):
-                outputs = ddp_model(inputs)
-                loss = criterion(outputs, labels)
-            with trace.trace_range("backward"):
-                loss.backward()
-            with trace.trace_range("optimizer"):
-                optimizer.step()
+            if graph_step is not None:
+                with trace.trace_range("step"):
+                    loss = graph_step(inputs, labels)
+            else:
+                optimizer.zero_grad()
+                with trace.trace_range("forward"), torch.autocast(device.type, torch.bfloat16,
+                                                                  enabled=autocast):
+                    outputs = ddp_model(inputs)
+                    loss = criterion(outputs, labels)
+                with trace.trace_range("backward"):
+                    loss.backward()
+                with trace.trace_range("optimizer"):
+                    optimizer.step()
             timer.tick()
             global_step += 1
             if args.log_every and (step + 1) % args.log_every == 0:

@@ -644,3 +644,22 @@ def test_relu_bitmask_dgrad_matches_z_mask(gpu, native_ext):
     g3, s3 = C.conv_dgrad_bn(dy, wt, [n, h, w_, c], 1, 0, addend, y, zm, stats, 3)
     assert torch.equal(g1, g3)
     assert torch.equal(s1, s3)
+
+
+def test_trainer_graph_matches_eager(gpu, native_ext, tmp_path):
+    """train.py --graph (HIP-graph replay of the whole step, eager warm-up and partial batches)
+    trains every batch exactly once: same weights as the eager trainer, bit for bit (the default
+    deterministic kernels), across an epoch boundary with a partial last batch and an evaluation.
+    The checkpoint is written at the start of each epoch, so the one of epoch 2 holds the state
+    after epochs 0 and 1."""
+    from pytorch_distributed_tutorials_amd.train import main
+    base = ["--arch", "resnet18", "--data", "synthetic-cifar", "--synthetic-samples", "200",
+            "--batch-size", "32", "--num_epochs", "3", "--eval-every", "1", "--num-classes", "10"]
+    sds = []
+    for extra, sub in (([], "eager"), (["--graph"], "graph")):
+        d = tmp_path / sub
+        assert main(base + extra + ["--model_dir", str(d)]) == 0
+        sds.append(torch.load(d / "resnet_distributed.pth", weights_only=True))
+    assert sds[0].keys() == sds[1].keys()
+    for k in sds[0]:
+        assert torch.equal(sds[0][k], sds[1][k]), k
