@@ -559,7 +559,10 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
   // then combine and store.  One exposed memory latency per batch instead of one per chunk (the
   // compiler cannot hoist a load above a store that may alias it); batches bound the registers.
   constexpr int IT_ALL = CHUNKS / 64;
-  constexpr int IT_MAX = 4;  // 4 x (y, z, addend) chunks in flight: occupancy stays as without batching
+#ifndef PDT_EPI_IT
+#define PDT_EPI_IT 8
+#endif
+  constexpr int IT_MAX = PDT_EPI_IT;  // (y, z, addend) chunks in flight per lane and batch
   constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
   static_assert(IT_ALL % IT == 0, "chunk batches");
   // The BN mask mode and the addend are wave-uniform: dispatch ONCE to a copy of the batch loop
