@@ -1,11 +1,12 @@
 """Failure detection and aux subsystems on CPU.
 
 * a rank that crashes mid-training makes the launcher fail fast (non-zero exit, no hang);
-* a rank that hangs inside training is detected by the other rank's progress watchdog,
+* a rank that hangs inside training is detected by a progress watchdog (its own or its peer's),
   which aborts with the watchdog exit code; the launcher then tears the job down;
 * unit checks of the watchdog, the fault-spec parser, step metrics and tracing."""
 import os
 import random
+import re
 import subprocess
 import sys
 import time
@@ -99,5 +100,7 @@ def test_rank_hang_detected_by_watchdog(tmp_path):
     r, dt = _launch(tmp_path, ["--max-steps-per-epoch", "6", "--watchdog-timeout", "8"],
                     PDT_FAULT="1:2:hang")
     assert r.returncode != 0
-    assert "[watchdog] rank 0: no progress" in r.stderr
+    # the hung rank and its blocked peer both stop progressing: whichever watchdog fires first
+    # aborts the job (the launcher then tears the other rank down)
+    assert re.search(r"\[watchdog\] rank [01]: no progress", r.stderr), r.stderr[-2000:]
     assert dt < 240
