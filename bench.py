@@ -48,6 +48,12 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--json-out", default=None)
+    p.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="process-group backend for N>1 (auto: nccl = RCCL when a GPU is present)")
+    p.add_argument("--share-device", action="store_true",
+                   help="rehearsal only: every rank runs on cuda:0 (needs --backend gloo; RCCL "
+                        "refuses two ranks on one device) so the N>1 bench path can be exercised "
+                        "on a one-GPU box")
     p.add_argument("--graph", action="store_true",
                    help="capture the whole training step in a HIP graph and replay it (native impl)")
     p.add_argument("--fp8", action="store_true",
@@ -82,9 +88,16 @@ def main(argv=None) -> int:
     from pytorch_distributed_tutorials_amd.optim import SGD
     from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel, init_distributed
 
-    env = init_distributed("nccl" if torch.cuda.is_available() else "gloo")
+    if args.share_device and args.backend != "gloo":
+        raise SystemExit("--share-device needs --backend gloo")
+    backend = args.backend if args.backend != "auto" else ("nccl" if torch.cuda.is_available() else "gloo")
+    env = init_distributed(backend)
     world = env.world_size
-    dev = torch.device(f"cuda:{env.local_rank}" if torch.cuda.is_available() else "cpu")
+    dev_index = 0 if args.share_device else env.local_rank
+    if torch.cuda.is_available():
+        torch.cuda.set_device(dev_index)
+    dev = torch.device(f"cuda:{dev_index}" if torch.cuda.is_available() else "cpu")
+    dev_ids = [dev_index] if dev.type == "cuda" else None
     torch.manual_seed(0)
 
     if args.fp8:
@@ -94,7 +107,7 @@ def main(argv=None) -> int:
     if args.impl == "native":
         model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
         model.set_impl("native")
-        ddp = DistributedDataParallel(model, device_ids=[env.local_rank], output_device=env.local_rank,
+        ddp = DistributedDataParallel(model, device_ids=dev_ids, output_device=dev_ids and dev_index,
                                       bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
         opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
         criterion = ops.CrossEntropyLoss()
@@ -104,8 +117,8 @@ def main(argv=None) -> int:
         model = build_model(args.arch, num_classes=args.num_classes, impl="torch").to(dev)
         model = model.to(memory_format=torch.channels_last)
         if world > 1:
-            ddp = nn.parallel.DistributedDataParallel(model, device_ids=[env.local_rank],
-                                                      output_device=env.local_rank,
+            ddp = nn.parallel.DistributedDataParallel(model, device_ids=dev_ids,
+                                                      output_device=dev_ids and dev_index,
                                                       bucket_cap_mb=args.bucket_mb)
         else:
             ddp = model
@@ -174,10 +187,12 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": (round(img_s / base, 4) if base else None),
             "dtype": "fp8" if args.fp8 else "bf16",
-            "data": "synthetic (ImageNet-shaped 3x224x224 fp32 images, random labels, random-init weights)",
+            "data": f"synthetic (ImageNet-shaped 3x{args.image_size}x{args.image_size} fp32 images, random labels, "
+                    "random-init weights)",
             "config": {"model": args.arch, "global_batch": args.batch * world,
                        "seq_len": None, "image_size": args.image_size,
                        "parallelism": f"dp{world}", "impl": args.impl,
+                       "backend": backend, "shared_device": bool(args.share_device),
                        "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype,
                        "cudnn_benchmark": bool(args.cudnn_benchmark), "graph": bool(args.graph),
                        "final_loss": round(final_loss, 4)},

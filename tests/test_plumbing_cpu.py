@@ -165,3 +165,29 @@ def test_cli_contract(monkeypatch):
     monkeypatch.setenv("RANK", "5")
     assert dist_env(None).local_rank == 5
     assert dist_env(1).local_rank == 1
+
+
+# ------------------------------------------------------------------ bench.py contract, N>1
+def test_bench_two_ranks_gloo(tmp_path):
+    """``bench.py --gpus 2`` self-launches torchrun, takes the max time over ranks and has rank 0
+    print one JSON line with the whole-job aggregate (driver contract)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_PORT=str(free_port()), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    out = tmp_path / "b.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--arch", "resnet18",
+                        "--image-size", "32", "--num-classes", "10", "--batch", "4", "--steps", "2",
+                        "--warmup", "1", "--impl", "torch", "--backend", "gloo", "--json-out", str(out)],
+                       cwd=root, env=env, timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d == json.loads(out.read_text())
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 8 and d["config"]["parallelism"] == "dp2"
+    assert abs(d["value"] - 8 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
