@@ -68,3 +68,14 @@ def test_ddp_native_model_path_cpu(tmp_path, native_ext):
     # rounding differences chaotically over steps; exact cross-rank equality still holds
     res = _run(tmp_path, ["--impl", "native", "--steps", "1"])
     _check(res, tol=1e-3, evals=1)
+
+
+@pytest.mark.slow
+def test_ddp_world8_native_reducer(tmp_path, native_ext):
+    # the world size of one MI355X node (reducer parity at 2 and 8 ranks):
+    # 8 gloo ranks, C++ reducer vs torch DDP, rank-0-only eval, bit-identical ranks
+    res = _run(tmp_path, ["--impl", "torch", "--steps", "2"], nproc=8, timeout=600)
+    _check(res)
+    assert len(res[0]["all_ranks_checksums"]) == 8
+    info = res[0]["bucket_info"]
+    assert res[0]["launch_order"] == list(range(info["num_buckets"]))
