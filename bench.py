@@ -26,6 +26,8 @@ import subprocess
 import sys
 import time
 
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see pytorch_distributed_tutorials_amd/__init__.py
+
 # Stock PyTorch-ROCm ResNet-50 bf16 (bench.py --impl torch --cudnn-benchmark: MIOpen with
 # solution search, hipBLASLt, autocast bf16, channels_last, foreach SGD) measured on one MI355X:
 # 6634.6 img/s (38.59 ms/step, 256 img/GPU).  The reference publishes no numbers, so

@@ -14,4 +14,12 @@ Layout:
   data/      DistributedSampler, synthetic device data, CIFAR-10
   utils/     env contract, seeding, checkpoints, profiling
 """
+import os as _os
+
+# Kernel arguments in device memory: the HIP runtime then skips the per-launch host-to-device
+# kernarg copy.  Measured on MI355X (profiles/r1s5_runtime_knobs.jsonl): host-bound ResNet-18 /
+# CIFAR step 87.3k -> 91.3k img/s, GPU-bound ResNet-50 step unchanged.  Read when the HIP
+# runtime initialises (first device call), so it must be set before that; set it to 0 to opt out.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 __version__ = "0.1.0"
