@@ -10,6 +10,7 @@
 #include "fp8_util.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <numeric>
 #include <stdexcept>
@@ -227,9 +228,25 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
 
 // grid of an 8-channel-vector elementwise pass: <= 8192 blocks of 256, rounded so that the grid
 // stride (blocks * 256) is a multiple of K8 -- every thread then keeps one channel group
-static int ew_blocks(int64_t nvec, int K8) {
+static int ew_block_cap_env() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_EW_BLOCKS");  // A/B knob: grid cap of every streaming BN pass
+    v = e ? std::max(256, atoi(e)) : 0;
+  }
+  return v;
+}
+
+// Grid caps measured per pass on MI355X (scripts/gpu_s5k.sh, 4096..32768): the residual-add
+// forward apply (2 reads + 1 write + mask per vector) is fastest with one vector per thread
+// (cap 32768: 102 -> 94.5 us per call), the other passes with 8192.
+constexpr int kEwCap = 8192;
+constexpr int kEwCapResidual = 32768;
+
+static int ew_blocks(int64_t nvec, int K8, int cap_default = kEwCap) {
   int64_t b = (nvec + 255) / 256;
-  b = b < 8192 ? b : 8192;
+  const int64_t cap = ew_block_cap_env() > 0 ? ew_block_cap_env() : cap_default;
+  b = b < cap ? b : cap;
   const int64_t q = K8 / std::gcd(K8, 256);
   return (int)(((b + q - 1) / q) * q);
 }
@@ -239,7 +256,7 @@ void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift
                        hipStream_t st, uint8_t* zmask) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
-  dim3 g(ew_blocks(nvec, K8)), b(256);
+  dim3 g(ew_blocks(nvec, K8, res ? kEwCapResidual : kEwCap)), b(256);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto R = reinterpret_cast<const uint4*>(res);
   auto Z = reinterpret_cast<uint4*>(z);
