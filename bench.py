@@ -48,6 +48,18 @@ def parse(argv=None):
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--impl", default="native", choices=["native", "torch"])
     p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--first-bucket-mb", type=float, default=1.0,
+                   help="cap of the bucket all-reduced first (torch DDP: 1 MiB)")
+    p.add_argument("--last-bucket-mb", type=float, default=None,
+                   help="cap of the bucket all-reduced LAST (stem/layer1 gradients; its all-reduce "
+                        "is the exposed tail). Default: no cap (torch DDP layout)")
+    p.add_argument("--force-comm", action="store_true",
+                   help="native impl: run the RCCL communicator + C++ reducer + buffer broadcasts "
+                        "even at N=1 (world-1 RCCL communicator; exercises the multi-GPU path)")
+    p.add_argument("--comm-timing", action="store_true",
+                   help="record all-reduce time / exposed tail per step (native RCCL path)")
+    p.add_argument("--deterministic", action="store_true",
+                   help="deterministic kernels (slab split-K weight gradients), the trainer's default")
     p.add_argument("--wire-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--json-out", default=None)
     p.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
@@ -101,6 +113,9 @@ def main(argv=None) -> int:
     dev = torch.device(f"cuda:{dev_index}" if torch.cuda.is_available() else "cpu")
     dev_ids = [dev_index] if dev.type == "cuda" else None
     torch.manual_seed(0)
+    if args.deterministic:
+        from pytorch_distributed_tutorials_amd.utils.seed import set_random_seeds
+        set_random_seeds(0, deterministic=True)
 
     if args.fp8:
         if args.impl != "native" or args.graph:
@@ -110,7 +125,12 @@ def main(argv=None) -> int:
         model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
         model.set_impl("native")
         ddp = DistributedDataParallel(model, device_ids=dev_ids, output_device=dev_ids and dev_index,
-                                      bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
+                                      bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
+                                      first_bucket_mb=args.first_bucket_mb,
+                                      last_bucket_mb=args.last_bucket_mb,
+                                      force_reducer=args.force_comm)
+        if args.comm_timing:
+            ddp.enable_comm_timing(True)
         opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
         criterion = ops.CrossEntropyLoss()
         autocast = None
@@ -162,8 +182,11 @@ def main(argv=None) -> int:
         loss = step()
     barrier()
     t0 = time.perf_counter()
+    host = 0.0  # host time spent inside step() (issue time; ~= step time when the host is the bound)
     for _ in range(args.steps):
+        th = time.perf_counter()
         loss = step()
+        host += time.perf_counter() - th
     barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -171,6 +194,13 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.item())
+    comm = None
+    if args.impl == "native":
+        info = ddp.bucket_info()
+        comm = {"native_comm": info["native_comm"], "reducer": info["reducer"],
+                "buckets_mb": [round(b / 2**20, 2) for b in info["bucket_bytes"]]}
+        if args.comm_timing:
+            comm["last_step"] = ddp.comm_stats()
 
     if env.rank == 0:
         img_s = world * args.batch * args.steps / elapsed
@@ -185,6 +215,7 @@ def main(argv=None) -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "host_ms_per_step": round(1000.0 * host / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(img_s / base, 4) if base else None),
@@ -197,7 +228,9 @@ def main(argv=None) -> int:
                        "backend": backend, "shared_device": bool(args.share_device),
                        "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype,
                        "cudnn_benchmark": bool(args.cudnn_benchmark), "graph": bool(args.graph),
-                       "final_loss": round(final_loss, 4)},
+                       "deterministic": bool(args.deterministic), "force_comm": bool(args.force_comm),
+                       "first_bucket_mb": args.first_bucket_mb, "last_bucket_mb": args.last_bucket_mb,
+                       "comm": comm, "final_loss": round(final_loss, 4)},
         }
         line = json.dumps(res)
         print(line, flush=True)

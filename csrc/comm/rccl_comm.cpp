@@ -2,6 +2,7 @@
 
 #include <c10/hip/HIPGuard.h>
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace pdt {
@@ -22,9 +23,19 @@ std::string RcclComm::unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
+// The comm stream is an ordinary-priority stream.  A high-priority stream was measured to cost
+// +16.5 ms per ResNet-50 step on MI355X (21.6 -> 38.1 ms, world-1 forced reducer) even with the
+// collectives skipped (PDT_REDUCER_SKIP_COLL=1: 38.0 ms): its event waits, not RCCL, stall the
+// compute queues.  PDT_COMM_HIGH_PRIORITY=1 restores it for A/B runs
+// (profiles/r2_comm_stream_priority_ab.md).
+static bool comm_high_priority() {
+  const char* e = std::getenv("PDT_COMM_HIGH_PRIORITY");
+  return e && e[0] == '1';
+}
+
 RcclComm::RcclComm(const std::string& uid, int rank, int world, int device)
     : rank_(rank), world_(world), device_(device),
-      stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)) {
+      stream_(c10::hip::getStreamFromPool(comm_high_priority(), (c10::DeviceIndex)device)) {
   if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("bad RCCL unique id size");
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   ncclUniqueId id;

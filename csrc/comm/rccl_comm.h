@@ -3,7 +3,7 @@
 // The reference gets its collectives from c10d's ProcessGroupNCCL
 // (init_process_group("nccl"), resnet/main.py:74).  Here the data-parallel hot
 // path talks to RCCL directly: the unique id is exchanged once through the
-// rendezvous store, every collective runs on a dedicated high-priority HIP
+// rendezvous store, every collective runs on a dedicated (normal-priority) HIP
 // stream, and compute<->comm ordering is expressed with HIP events so gradient
 // all-reduces overlap the remaining backward kernels.  On an 8x MI355X node the
 // transport is xGMI (7 point-to-point links per GPU); RCCL picks rings/trees

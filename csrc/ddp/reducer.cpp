@@ -40,6 +40,9 @@ struct ReducerState {
   // wrote into memory an in-flight collective reads -> error instead of a silent race
   bool strict = false;
   int64_t duplicate_marks = 0;
+  // diagnostics only (PDT_REDUCER_SKIP_COLL=1): keep every stream wait/event of the RCCL path
+  // but issue no collective -- separates RCCL's own cost from the ordering's cost
+  bool skip_collectives = false;
   // side stream that produces some gradients (weight-gradient GEMMs run there, concurrent with
   // the input-gradient chain): every bucket all-reduce also waits for it
   hipStream_t aux = nullptr;
@@ -87,7 +90,7 @@ struct ReducerState {
         float scale = average ? 1.f / (float)comm->world() : 1.f;
         launch_cast_bf16_f32(reinterpret_cast<const uint16_t*>(wire[b].data_ptr()),
                              f.data_ptr<float>(), f.numel(), scale, cs);
-      } else {
+      } else if (!skip_collectives) {
         comm->all_reduce_raw(f.data_ptr(), (size_t)f.numel(), RcclComm::dtype_of(f),
                              average ? ncclAvg : ncclSum);
       }
@@ -209,6 +212,7 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   }
   st_->reset_counters();
   if (const char* e = std::getenv("PDT_DEBUG_REDUCER")) st_->strict = e[0] == '1';
+  if (const char* e = std::getenv("PDT_REDUCER_SKIP_COLL")) st_->skip_collectives = e[0] == '1';
 
   std::weak_ptr<ReducerState> weak = st_;
   st_->self = weak;
@@ -218,7 +222,13 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
     int64_t idx = (int64_t)i;
     acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
         [weak, idx](const torch::autograd::variable_list& outputs,
-                    const torch::autograd::variable_list& /*inputs*/) {
+                    const torch::autograd::variable_list& inputs) {
+          // The engine runs AccumulateGrad -- and its post hooks -- even when the gradient that
+          // reaches it is undefined.  That is the case for every parameter a fused native
+          // backward accumulated in place into its flat view (it returns None to autograd and
+          // calls mark_ready_external itself, BEFORE this node runs) and for parameters unused
+          // this iteration (finalize handles them).  Neither is a readiness event.
+          if (!inputs.empty() && !inputs[0].defined()) return outputs;
           if (auto s = weak.lock()) s->on_ready(idx);
           return outputs;
         }));

@@ -9,7 +9,9 @@ from .fused import (  # noqa: F401
     CrossEntropyLoss,
     act_dtype,
     avgpool_linear,
+    buffers_ready,
     bump_bn_counters,
+    defer_buffer_wait,
     conv_bn,
     cross_entropy,
     fp8_attach,

@@ -162,6 +162,7 @@ class _ConvBN(torch.autograd.Function):
             C = native()
             wk = C.pack_weight(weight, cx)                       # bf16 [K,R,S,Cx]
             y, part = C.conv_fwd(x, wk, stride, pad, training)    # bf16 NHWC + tile stats
+            buffers_ready()
             if training:
                 if running_mean is None:  # track_running_stats=False: updates go to scratch
                     running_mean = torch.zeros(k, device=x.device)
@@ -239,6 +240,7 @@ class _StemConvBN(torch.autograd.Function):
         xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
         k = weight.shape[0]
         count = y.shape[0] * y.shape[1] * y.shape[2]
+        buffers_ready()
         if training:
             if running_mean is None:
                 running_mean = torch.zeros(k, device=x.device)
@@ -293,6 +295,7 @@ class _StemConvBNPool(torch.autograd.Function):
         xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
         k = weight.shape[0]
         count = y.shape[0] * y.shape[1] * y.shape[2]
+        buffers_ready()
         if training:
             if running_mean is None:
                 running_mean = torch.zeros(k, device=x.device)
@@ -479,12 +482,40 @@ def top1_correct(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 _NBT_BATCHED = 0  # > 0 inside bump_bn_counters(): the counters were already bumped in one launch
 
+# BN buffers arriving from the DDP per-forward broadcast (torch DDP's _sync_buffers,
+# torch/nn/parallel/distributed.py:1557): the broadcast runs on the comm stream and only the
+# BatchNorm statistics kernels read/write those buffers, so the compute stream waits for it
+# at the FIRST BN of the forward (after the stem convolution has been issued), not before the
+# forward starts.  The counter bump writes the same (int64) flat buffer, so it is deferred too.
+_BUFFER_WAIT = None   # callable: current stream waits for the buffer broadcast
+_PENDING_BUMP = None  # num_batches_tracked tensors to bump once the buffers are ours
+
+
+def defer_buffer_wait(fn) -> None:
+    """Register the stream wait for an in-flight buffer broadcast (called by DDP)."""
+    global _BUFFER_WAIT
+    _BUFFER_WAIT = fn
+
+
+def buffers_ready() -> None:
+    """Make BN buffers safe to use on the current stream: run the deferred broadcast wait and
+    the deferred counter bump (no-ops when nothing is pending)."""
+    global _BUFFER_WAIT, _PENDING_BUMP
+    if _BUFFER_WAIT is not None:
+        fn, _BUFFER_WAIT = _BUFFER_WAIT, None
+        fn()
+    if _PENDING_BUMP is not None:
+        counters, _PENDING_BUMP = _PENDING_BUMP, None
+        with torch.no_grad():
+            torch._foreach_add_(counters, 1)
+
 
 class bump_bn_counters:
     """Context for one device forward of a whole model: bumps every training BatchNorm's
     ``num_batches_tracked`` (torch BN semantics) with ONE multi-tensor launch
     instead of one ``add_`` kernel per BN (53 launches per ResNet-50 step); the per-BN
-    ``_bn_prepare`` calls inside the context then skip their own bump."""
+    ``_bn_prepare`` calls inside the context then skip their own bump.  The launch itself is
+    issued by the first BN of the forward (``buffers_ready``), behind any buffer broadcast."""
 
     def __init__(self, module: nn.Module):
         self.counters = [m.num_batches_tracked for m in module.modules()
@@ -492,16 +523,16 @@ class bump_bn_counters:
                          and m.track_running_stats and m.num_batches_tracked is not None]
 
     def __enter__(self):
-        global _NBT_BATCHED
+        global _NBT_BATCHED, _PENDING_BUMP
         if self.counters:
-            with torch.no_grad():
-                torch._foreach_add_(self.counters, 1)
+            _PENDING_BUMP = self.counters
         _NBT_BATCHED += 1
         return self
 
     def __exit__(self, *exc):
         global _NBT_BATCHED
         _NBT_BATCHED -= 1
+        buffers_ready()  # a forward without BatchNorm still owes the wait and the bump
         return False
 
 
@@ -557,6 +588,7 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
         m = _mirror_of(w)
         _nan_trace(f"unit_fwd {tuple(x.shape)}->{tuple(y.shape)} mirror={m is not None and m.krsc_view(w) is wk}",
                    x=x, wk=wk, y=y, part=part)
+    buffers_ready()
     if training:
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:

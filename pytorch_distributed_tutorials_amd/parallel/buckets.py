@@ -17,7 +17,7 @@ backward, whose all-reduce cannot overlap anything) matter more than the cap.
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 MiB = 1 << 20
 
@@ -46,11 +46,70 @@ def plan_buckets(sizes_bytes: Sequence[int], caps_bytes: Sequence[int]) -> List[
     return out
 
 
+def split_tail(plan: List[List[int]], sizes_bytes: Sequence[int], last_cap_bytes: int) -> List[List[int]]:
+    """Cap the LAST bucket: carve the trailing items (in readiness order) whose total stays
+    within ``last_cap_bytes`` into a final bucket of their own.  The item that would cross the
+    cap stays in the previous bucket, so the tail bucket is <= the cap unless its single last
+    item alone exceeds it (then that item is the tail).  ``plan`` holds positions."""
+    if not plan or last_cap_bytes <= 0:
+        return plan
+    last = plan[-1]
+    total = sum(int(sizes_bytes[p]) for p in last)
+    if total <= last_cap_bytes or len(last) == 1:
+        return plan
+    tail: List[int] = []
+    acc = 0
+    for p in reversed(last):
+        if tail and acc + int(sizes_bytes[p]) > last_cap_bytes:
+            break
+        tail.append(p)
+        acc += int(sizes_bytes[p])
+    tail.reverse()
+    head = last[:len(last) - len(tail)]
+    return plan[:-1] + ([head] if head else []) + [tail]
+
+
 def ddp_bucket_plan(param_sizes_bytes: Sequence[int], bucket_cap_mb: float = 25.0,
-                    first_bucket_mb: float = 1.0) -> List[List[int]]:
-    """Buckets of parameter INDICES (definition order) in reverse-definition order."""
+                    first_bucket_mb: float = 1.0,
+                    last_bucket_mb: Optional[float] = None) -> List[List[int]]:
+    """Buckets of parameter INDICES (definition order) in reverse-definition order.
+
+    ``first_bucket_mb`` caps the bucket launched first (torch: 1 MiB); ``last_bucket_mb``
+    (None = torch behaviour, no cap) caps the bucket launched LAST -- the one holding the
+    stem/layer1 gradients, produced at the very end of backward, whose all-reduce is the only
+    one nothing can hide (see ``tail_time_us``)."""
     n = len(param_sizes_bytes)
     order = list(reversed(range(n)))
     caps = [int(first_bucket_mb * MiB), int(bucket_cap_mb * MiB)]
-    plan = plan_buckets([param_sizes_bytes[i] for i in order], caps)
+    sizes = [param_sizes_bytes[i] for i in order]
+    plan = plan_buckets(sizes, caps)
+    if last_bucket_mb is not None:
+        plan = split_tail(plan, sizes, int(last_bucket_mb * MiB))
     return [[order[p] for p in b] for b in plan]
+
+
+# ---------------------------------------------------------------------------------------------
+# xGMI tail model
+# ---------------------------------------------------------------------------------------------
+XGMI_LINK_GBPS = 153.0   # one xGMI link, one direction (MI355X, 8-GPU node)
+XGMI_LINKS = 7           # point-to-point links per GPU in a fully connected 8-GPU node
+RCCL_LAUNCH_US = 12.0    # per-collective fixed cost (launch + ring setup), order of magnitude
+
+
+def allreduce_us(nbytes: int, world: int, links_used: int = 1, latency_us: float = RCCL_LAUNCH_US,
+                 link_gbps: float = XGMI_LINK_GBPS) -> float:
+    """Analytic all-reduce time: a ring moves 2(n-1)/n of the buffer over each GPU's busiest
+    link; RCCL's channels spread that over ``links_used`` of the 7 links (1 = a single ring,
+    7 = every link busy).  Returns microseconds."""
+    if world <= 1:
+        return latency_us
+    wire = 2.0 * (world - 1) / world * nbytes
+    return latency_us + wire / (links_used * link_gbps * 1e3)
+
+
+def tail_time_us(plan_bytes: Sequence[int], world: int, links_used: int = 1) -> float:
+    """Exposed all-reduce time after the last gradient is produced: the last bucket's
+    all-reduce cannot overlap any backward kernel (everything before it can)."""
+    if not plan_bytes:
+        return 0.0
+    return allreduce_us(int(plan_bytes[-1]), world, links_used)

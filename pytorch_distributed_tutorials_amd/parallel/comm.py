@@ -10,7 +10,7 @@ configurable.  On ROCm the ``nccl`` backend is RCCL.
 ``csrc/comm/rccl_comm.cpp``) for the data-parallel hot path: rank 0 draws the
 RCCL unique id and publishes it through the rendezvous store -- the store is
 the only thing shared with c10d; every gradient/buffer collective afterwards is
-issued from C++ on a dedicated high-priority HIP stream.
+issued from C++ on a dedicated (normal-priority) HIP stream.
 """
 from __future__ import annotations
 
@@ -62,12 +62,23 @@ def backend_name(pg=None) -> str:
 
 
 def native_comm(device: torch.device, pg=None):
-    """The RCCL communicator of this process for ``pg`` (cached)."""
+    """The RCCL communicator of this process for ``pg`` (cached).
+
+    Without an initialised process group (a single-process run) this is a world-1 RCCL
+    communicator whose unique id never leaves the process: every collective of the
+    data-parallel path still runs through RCCL (the forced-reducer mode of
+    ``DistributedDataParallel``, used to execute and test that path on one GPU)."""
     from ..ops._ext import native
     key = (id(pg), device.index)
     if key in _COMM_CACHE:
         return _COMM_CACHE[key]
     C = native()
+    if not (dist.is_available() and dist.is_initialized()):
+        if pg is not None:
+            raise RuntimeError("native_comm: a process group was given but none is initialised")
+        comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1, device.index)
+        _COMM_CACHE[key] = comm
+        return comm
     store = dist.distributed_c10d._get_default_store()
     ws = dist.get_world_size(pg)
     rk = dist.get_rank(pg)

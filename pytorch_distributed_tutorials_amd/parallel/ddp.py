@@ -21,13 +21,14 @@ MI355X-specific design:
     contiguous slices; buffers are flattened too, so the per-forward buffer
     broadcast is ONE RCCL call per dtype;
   * the reducer is native C++ (``csrc/ddp/reducer.cpp``) driving our own RCCL
-    communicator on a high-priority side stream (``comm.native_comm``) with
+    communicator on a side stream (``comm.native_comm``) with
     ncclAvg, optionally bf16 on the wire; on CPU/gloo the same C++ reducer calls
     back into ``torch.distributed``.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional
 
 import torch
@@ -138,7 +139,8 @@ class DistributedDataParallel(nn.Module):
                  output_device=None, broadcast_buffers: bool = True, process_group=None,
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
-                 comm: str = "auto", wire_dtype: str = "fp32", average: bool = True):
+                 comm: str = "auto", wire_dtype: str = "fp32", average: bool = True,
+                 last_bucket_mb: Optional[float] = None, force_reducer: bool = False):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -147,10 +149,17 @@ class DistributedDataParallel(nn.Module):
         self.process_group = process_group
         self.bucket_cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
         self.first_bucket_mb = first_bucket_mb
+        self.last_bucket_mb = last_bucket_mb
         self.find_unused_parameters = find_unused_parameters  # unused params are zero-filled
         self.average = average
         self.world_size = pcomm.world_size()
         self.rank = pcomm.rank()
+        # force_reducer: run the whole collective path (communicator, reducer, bucket
+        # all-reduces, buffer broadcasts) even in a single process -- a world-1 RCCL
+        # communicator makes every collective an identity, so one GPU executes and tests the
+        # exact code the multi-GPU runs use
+        self.force_reducer = bool(force_reducer)
+        self._collective = self.world_size > 1 or self.force_reducer
         self.require_forward_param_sync = True
         self.require_backward_grad_sync = True
 
@@ -164,7 +173,7 @@ class DistributedDataParallel(nn.Module):
 
         # ---- flat layout in bucket order
         sizes = [p.numel() * p.element_size() for p in params]
-        plan = ddp_bucket_plan(sizes, self.bucket_cap_mb, self.first_bucket_mb)
+        plan = ddp_bucket_plan(sizes, self.bucket_cap_mb, self.first_bucket_mb, self.last_bucket_mb)
         layout = [i for b in plan for i in b]
         self.space = FlatParamSpace([params[i] for i in layout])
         self.bucket_ranges = []
@@ -175,25 +184,32 @@ class DistributedDataParallel(nn.Module):
             end = self.space.offsets[pos] if pos < len(layout) else self.space.numel
             self.bucket_ranges.append((start, end))
         self.bucket_sizes = [e - s for s, e in self.bucket_ranges]
+        self.bucket_bytes = [n * self.space.param_flat.element_size() for n in self.bucket_sizes]
         self.buffer_flats = flatten_buffers(module)
 
         # ---- communicator
         self.comm = None
         be = pcomm.backend_name(process_group)
-        use_native = (comm in ("auto", "rccl") and self.device.type == "cuda" and be == "nccl"
-                      and native_available())
+        single = be == "none" and self.force_reducer  # no process group: world-1 RCCL comm
+        use_native = (comm in ("auto", "rccl") and self.device.type == "cuda"
+                      and (be == "nccl" or single) and native_available())
         if comm == "rccl" and not use_native:
-            raise RuntimeError("comm='rccl' needs a CUDA device, the nccl backend and the native extension")
-        if self.world_size > 1 and use_native:
+            raise RuntimeError("comm='rccl' needs a CUDA device, the nccl backend (or force_reducer "
+                               "in a single process) and the native extension")
+        if self._collective and use_native:
             self.comm = pcomm.native_comm(self.device, process_group)
+        # the buffer-broadcast wait can move to the first BatchNorm only where every buffer
+        # reader is one of our BN kernels (ops.buffers_ready): the native device model
+        self._defer_buffer_wait = (self.comm is not None and getattr(module, "impl", None) == "native"
+                                   and os.environ.get("PDT_DEFER_BUFFER_WAIT", "1") != "0")
 
-        if self.world_size > 1:
+        if self._collective and (self.world_size > 1 or self.comm is not None):
             self._sync_module_states()
 
         # ---- reducer
         self.reducer = None
         self._works = []
-        if self.world_size > 1:
+        if self._collective:
             bucket_of = []
             for bi, b in enumerate(plan):
                 bucket_of.extend([bi] * len(b))
@@ -252,25 +268,33 @@ class DistributedDataParallel(nn.Module):
             for flat in self.buffer_flats.values():
                 self._broadcast(flat)
             if self.comm is not None:
-                self.comm.current_wait_comm()
+                if self._defer_buffer_wait:
+                    from .. import ops
+                    ops.defer_buffer_wait(self.comm.current_wait_comm)
+                else:
+                    self.comm.current_wait_comm()
 
     # called from the C++ reducer for non-RCCL backends
     def _py_launch(self, b: int) -> None:
-        self._works.append(dist.all_reduce(self._flats[b], group=self.process_group, async_op=True))
+        if self.world_size > 1:
+            self._works.append(dist.all_reduce(self._flats[b], group=self.process_group, async_op=True))
 
     def _py_finalize(self) -> None:
         for w in self._works:
             w.wait()
         self._works = []
-        if self.average:
+        if self.average and self.world_size > 1:
             self.space.grad_flat.div_(self.world_size)
 
     # ------------------------------------------------------------- API
     def forward(self, *inputs, **kwargs):
-        if self.world_size > 1 and self.broadcast_buffers and self.require_forward_param_sync \
-                and self.buffer_flats:
+        if self._collective and self.broadcast_buffers and self.require_forward_param_sync \
+                and self.buffer_flats and (self.world_size > 1 or self.comm is not None):
             self._sync_buffers()
         out = self.module(*inputs, **kwargs)
+        if self._defer_buffer_wait:
+            from .. import ops
+            ops.buffers_ready()  # normally already consumed by the first BatchNorm
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.require_forward_param_sync = True
             if self.reducer is not None:
@@ -313,5 +337,6 @@ class DistributedDataParallel(nn.Module):
 
     def bucket_info(self) -> dict:
         return {"num_buckets": len(self.bucket_ranges), "bucket_elems": list(self.bucket_sizes),
-                "native_comm": self.comm is not None,
+                "bucket_bytes": list(self.bucket_bytes),
+                "native_comm": self.comm is not None, "forced": self.force_reducer,
                 "reducer": type(self.reducer).__name__ if self.reducer is not None else None}

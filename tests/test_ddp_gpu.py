@@ -4,8 +4,9 @@ RCCL cannot put two ranks on one device, and gpurun boxes have one GPU, so this
 exercises everything of the multi-GPU path except RCCL itself: native kernels,
 in-place gradient sinks, the side-stream weight gradients the reducer must join
 before each bucket's collective, bucket ordering and the fused optimizer.  The
-RCCL communicator is covered by test_kernels_gpu.py::test_rccl_comm_single_rank
-and by the driver's 8-GPU scaling run.
+RCCL communicator + C++ reducer path itself is executed on one GPU by
+test_rccl_gpu.py (forced world-1 communicator: bitwise gradients, bf16 wire,
+timing, launch order, strict duplicate-mark checking).
 """
 import json
 import os

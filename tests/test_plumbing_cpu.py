@@ -62,6 +62,60 @@ def test_resnet50_bucket_sizes_from_survey():
         [2049000, 7875584, 6563840, 6637568, 2431040]
 
 
+def test_last_bucket_cap_hand_layout():
+    MiB = 1 << 20
+    # definition order sizes 1..6 MiB -> readiness order 6,5,4,3,2,1 MiB; caps [1, 8] MiB:
+    # [6] | [5,4] | [3,2,1]; a 3 MiB tail cap carves [2,1] off the last bucket
+    sizes = [k * MiB for k in range(1, 7)]
+    assert ddp_bucket_plan(sizes, 8.0, 1.0) == [[5], [4, 3], [2, 1, 0]]
+    assert ddp_bucket_plan(sizes, 8.0, 1.0, last_bucket_mb=3.0) == [[5], [4, 3], [2], [1, 0]]
+    # a tail cap at or above the last bucket changes nothing; one oversized item stays alone
+    assert ddp_bucket_plan(sizes, 8.0, 1.0, last_bucket_mb=6.0) == [[5], [4, 3], [2, 1, 0]]
+    assert ddp_bucket_plan(sizes, 8.0, 1.0, last_bucket_mb=0.5) == [[5], [4, 3], [2, 1], [0]]
+
+
+def test_resnet50_tail_bucket_and_model():
+    from pytorch_distributed_tutorials_amd.parallel.buckets import allreduce_us, tail_time_us
+    m = build_model("resnet50")
+    params = list(m.parameters())
+    sizes = [p.numel() * 4 for p in params]
+    base = ddp_bucket_plan(sizes)
+    capped = ddp_bucket_plan(sizes, last_bucket_mb=2.0)
+    # same readiness order (the flat layout does not move), only the tail is split
+    assert [i for b in base for i in b] == [i for b in capped for i in b]
+    assert len(capped) == len(base) + 1
+    tail = sum(sizes[i] for i in capped[-1])
+    assert tail <= 2 << 20
+    # the exposed tail shrinks with the cap; a 1-link ring is 7x slower than all links
+    t_base = tail_time_us([sum(sizes[i] for i in b) for b in base], 8)
+    t_cap = tail_time_us([sum(sizes[i] for i in b) for b in capped], 8)
+    assert t_cap < t_base
+    big = 100 << 20
+    assert allreduce_us(big, 8, 1, latency_us=0) == pytest.approx(7 * allreduce_us(big, 8, 7, latency_us=0))
+    # 2(n-1)/n * 102.2 MB over one 153 GB/s link = 1.17 ms
+    assert allreduce_us(102_228_128, 8, 1, latency_us=0) == pytest.approx(1169, rel=1e-2)
+
+
+def test_forced_reducer_world1_cpu(native_ext):
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    assert not (dist.is_available() and dist.is_initialized())
+    x = torch.randn(4, 3, 32, 32)
+    y = torch.randint(0, 10, (4,))
+    res = []
+    for force in (False, True):
+        torch.manual_seed(0)
+        m = build_model("resnet18", num_classes=10)
+        ddp = DistributedDataParallel(m, force_reducer=force, last_bucket_mb=1.0)
+        assert (ddp.reducer is not None) == force
+        nn.functional.cross_entropy(ddp(x), y).backward()
+        res.append(ddp.space.grad_flat.clone())
+        if force:
+            nb = ddp.reducer.num_buckets
+            assert ddp.reducer.last_launch_order() == list(range(nb))
+            assert ddp.bucket_info()["forced"]
+    assert torch.equal(res[0], res[1])
+
+
 # -------------------------------------------------------------------- model
 @pytest.mark.parametrize("arch,count,keys", [("resnet18", 11689512, 122), ("resnet50", 25557032, 320),
                                              ("resnet152", 60192808, 932)])

@@ -1,0 +1,166 @@
+"""The RCCL data-parallel path executed on ONE GPU (forced world-1 communicator).
+
+The multi-GPU hot path -- our C++ ``Reducer`` launching bucket all-reduces on our own RCCL
+communicator (``csrc/ddp/reducer.cpp``, ``csrc/comm/rccl_comm.cpp``), the bf16 wire format,
+``ncclAvg``, the side-stream join before each bucket, the comm-timing events and the per-forward
+BN-buffer broadcast with its deferred wait -- is what the reference's ``init_process_group("nccl")``
++ DDP wrap + overlapped all-reduce (``resnet/main.py:74,80,123``) become here.  A single-process
+``DistributedDataParallel(force_reducer=True)`` runs all of it through a world-1 RCCL
+communicator, where every collective is an identity: the gradients must be BITWISE those of the
+same model without the reducer (deterministic kernels), bf16 on the wire must stay within bf16
+rounding, and the bookkeeping (launch order, duplicate marks, timing) must be exact.
+"""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _build(dev, arch="resnet50", force=False, wire="fp32", last_mb=None, seed=0):
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.optim import SGD
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    torch.manual_seed(seed)
+    m = build_model(arch, num_classes=1000, impl="native").to(dev)
+    m.set_impl("native")
+    ddp = DistributedDataParallel(m, device_ids=[dev.index], output_device=dev.index,
+                                  comm="rccl" if force else "auto", force_reducer=force,
+                                  wire_dtype=wire, last_bucket_mb=last_mb)
+    opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+    return ddp, opt
+
+
+def _data(dev, n=16, hw=112):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, 3, hw, hw, generator=g).to(dev)
+    y = torch.randint(0, 1000, (n,), generator=g).to(dev)
+    return x, y
+
+
+def _train(ddp, opt, x, y, steps=2):
+    from pytorch_distributed_tutorials_amd import ops
+    grads, losses = [], []
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = ops.cross_entropy(ddp(x), y)
+        loss.backward()
+        grads.append(ddp.space.grad_flat.clone())
+        losses.append(float(loss.item()))
+        opt.step()
+    torch.cuda.synchronize()
+    bufs = {str(k): v.clone() for k, v in ddp.buffer_flats.items()}
+    return grads, losses, ddp.space.param_flat.clone(), bufs
+
+
+@pytest.fixture
+def det():
+    from pytorch_distributed_tutorials_amd.utils import seed
+    seed.set_random_seeds(0, deterministic=True)   # slab split-K weight gradients: bitwise repeatable
+    yield
+    seed.set_random_seeds(0, deterministic=False)
+
+
+def test_forced_reducer_fp32_wire_bitwise(gpu, det):
+    x, y = _data(gpu)
+    ddp0, opt0 = _build(gpu, force=False)
+    assert ddp0.reducer is None and ddp0.comm is None
+    ref = _train(ddp0, opt0, x, y)
+    del ddp0, opt0
+
+    ddp1, opt1 = _build(gpu, force=True)
+    info = ddp1.bucket_info()
+    assert info["native_comm"] and info["reducer"] == "Reducer" and info["forced"]
+    assert ddp1.enable_comm_timing(True)
+    ddp1.reducer.set_strict(True)     # a gradient marked again after its all-reduce raises
+    got = _train(ddp1, opt1, x, y)
+
+    for s in range(2):
+        assert torch.equal(ref[0][s], got[0][s]), f"step {s}: gradients differ through the reducer"
+        assert ref[1][s] == got[1][s]
+    assert torch.equal(ref[2], got[2]), "parameters differ after two SGD steps"
+    for k in ref[3]:
+        assert torch.equal(ref[3][k], got[3][k]), f"BN buffers ({k}) differ"
+    nb = ddp1.reducer.num_buckets
+    assert nb == len(ddp1.bucket_sizes) > 1
+    assert ddp1.reducer.last_launch_order() == list(range(nb))
+    assert ddp1.reducer.duplicate_marks == 0
+    assert ddp1.reducer.iterations == 2
+    st = ddp1.comm_stats()
+    assert st is not None and math.isfinite(st["comm_ms"]) and math.isfinite(st["exposed_ms"])
+    assert st["comm_ms"] >= 0 and 0 <= st["exposed_ms"] <= st["comm_ms"] + 1e-3
+
+
+def test_forced_reducer_bf16_wire(gpu, det):
+    x, y = _data(gpu)
+    ddp0, opt0 = _build(gpu, force=True, wire="fp32")
+    ref = _train(ddp0, opt0, x, y, steps=1)
+    del ddp0, opt0
+    ddp1, opt1 = _build(gpu, force=True, wire="bf16")
+    got = _train(ddp1, opt1, x, y, steps=1)
+    g0, g1 = ref[0][0], got[0][0]
+    rel = float((g1 - g0).norm() / g0.norm())
+    assert rel < 1e-2, rel
+    # bf16 on the wire: every gradient element is a bf16 value (round trip of the wire copy)
+    assert torch.equal(g1, g1.to(torch.bfloat16).float())
+    assert not torch.equal(g0, g1)  # the wire copy really was bf16
+    assert ddp1.reducer.last_launch_order() == list(range(ddp1.reducer.num_buckets))
+
+
+def test_last_bucket_cap_layout_and_grads(gpu, det):
+    x, y = _data(gpu, n=8, hw=64)
+    ddp0, opt0 = _build(gpu, force=True)
+    ref = _train(ddp0, opt0, x, y, steps=1)
+    n0 = ddp0.reducer.num_buckets
+    del ddp0, opt0
+    ddp1, opt1 = _build(gpu, force=True, last_mb=1.0)
+    got = _train(ddp1, opt1, x, y, steps=1)
+    assert ddp1.reducer.num_buckets == n0 + 1
+    assert ddp1.bucket_bytes[-1] <= 1 << 20
+    assert ddp1.reducer.last_launch_order() == list(range(n0 + 1))
+    # splitting the tail keeps the readiness order, so the flat layout is unchanged
+    assert torch.equal(ref[0][0], got[0][0])
+
+
+def test_rccl_world1_collectives(gpu, native_ext):
+    from pytorch_distributed_tutorials_amd.parallel import comm as pcomm
+    c = pcomm.native_comm(gpu)
+    assert c.world == 1 and c.rank == 0
+    x = torch.randn(4096, device=gpu)
+    out = torch.empty(4096, device=gpu)
+    c.reduce_scatter(x, out, "sum")
+    back = torch.empty(4096, device=gpu)
+    c.all_gather(out, back)
+    c.all_reduce(back, "avg")
+    c.broadcast(back, 0)
+    c.current_wait_comm()
+    torch.cuda.synchronize()
+    assert torch.equal(back, x)
+    xb = x.to(torch.bfloat16)
+    c.all_reduce(xb, "max")
+    c.current_wait_comm()
+    assert torch.equal(xb, x.to(torch.bfloat16))
+    c.barrier()
+
+
+def test_bench_force_comm_json(gpu, tmp_path):
+    out = tmp_path / "b.json"
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-comm", "--comm-timing",
+           "--steps", "2", "--warmup", "1", "--batch", "16", "--image-size", "64",
+           "--last-bucket-mb", "2", "--json-out", str(out)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=110, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    cfg = res["config"]
+    assert cfg["force_comm"] and cfg["comm"]["native_comm"] and cfg["comm"]["reducer"] == "Reducer"
+    assert cfg["comm"]["buckets_mb"][-1] <= 2.0
+    assert cfg["comm"]["last_step"] is not None
+    assert res["value"] > 0 and math.isfinite(cfg["final_loss"])
