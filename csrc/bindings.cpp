@@ -992,6 +992,25 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fmt_a") = 0, py::arg("fmt_b") = 0, py::arg("scale_a") = 127, py::arg("scale_b") = 127,
         py::arg("use_scale") = true);
   m.def("conv_nt_group_rows", &pdt::conv_nt_group_rows, py::arg("M"), py::arg("Nout"), py::arg("kg_bytes"));
+  m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
+    int bm = 0, bn = 0;
+    pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);
+    return py::make_tuple(bm, bn);
+  }, py::arg("M"), py::arg("Nout"), py::arg("kg_bytes"));
+  m.def("conv_wgrad_plan", [](std::vector<int64_t> x_shape, std::vector<int64_t> w_shape, int stride, int pad,
+                              bool deterministic) {
+    TORCH_CHECK(x_shape.size() == 4 && w_shape.size() == 4, "x_shape [N,H,W,C], w_shape [K,C,R,S]");
+    pdt::ConvShape s{};
+    s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.C = (int)x_shape[3];
+    s.K = (int)w_shape[0]; s.R = (int)w_shape[2]; s.S = (int)w_shape[3];
+    s.stride = stride; s.pad = pad;
+    s.Ho = (s.H + 2 * pad - s.R) / stride + 1; s.Wo = (s.W + 2 * pad - s.S) / stride + 1;
+    int out[4];
+    pdt::conv_wgrad_plan(s, deterministic, out);
+    py::dict d;
+    d["bm"] = out[0]; d["bn"] = out[1]; d["tiles"] = out[2]; d["splits"] = out[3];
+    return d;
+  }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("deterministic") = false);
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });
 

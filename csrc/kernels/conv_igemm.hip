@@ -1126,6 +1126,16 @@ int conv_nt_group_rows(int M, int Nout, int kg_bytes) {
   return use_wide_tile(M, Nout, kg_bytes) ? 256 : 128;
 }
 
+// Introspection for tests: (BM, BN) of the bf16 NT tile dispatch_nt runs for a GEMM of M rows,
+// Nout columns and a B-row length of kg_bytes (fp8 uses the same rule on its byte length).
+void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn) {
+  const int rows = conv_nt_group_rows(M, Nout, kg_bytes);
+  if (Nout <= 64) { *bm = 256; *bn = 64; }
+  else if (rows == 64) { *bm = 64; *bn = 128; }
+  else if (rows == 256) { *bm = 256; *bn = 256; }
+  else { *bm = 128; *bn = 128; }
+}
+
 template <bool C64, int EPI, int OP = OP_BF16>
 static void dispatch_nt(const NtArgs& a, hipStream_t st) {
   const int rows = conv_nt_group_rows(a.M, a.Nout, a.Kg * (OP == OP_BF16 ? 2 : 1));
@@ -1349,6 +1359,11 @@ static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   return p;
+}
+
+void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]) {
+  const WgradPlan p = plan_wgrad(s, deterministic);
+  out[0] = p.bmg; out[1] = p.bng; out[2] = p.tiles; out[3] = p.splits;
 }
 
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {

@@ -50,6 +50,8 @@ struct ConvShape {
 // BN partials part[ceil(M/G)][2][K] = (sum, M2 about the group mean), G = conv_nt_group_rows(M, K,
 // R*S*C*elem_bytes) = the BM of the workgroup tile the launch uses (one group per row tile).
 int conv_nt_group_rows(int M, int Nout, int kg_bytes);
+// (BM, BN) of the NT workgroup tile the fwd / dgrad launch of such a GEMM runs (test introspection)
+void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
                      const ConvShape& s, hipStream_t st);
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);
@@ -73,6 +75,8 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
+// the weight-gradient launch plan: {tile rows (output channels), tile cols, tiles, split-K factor}
+void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]);
 // accumulate: dw += wgrad (autograd accumulation semantics; lets the block write straight into
 // the flat gradient buffer), else dw = wgrad.
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,

@@ -6,7 +6,7 @@
 # Every step runs under its own `timeout -k 10`, logs to gpurun_out/TAG_<step>.log and appends
 # "<step> rc=N" to gpurun_out/TAG_status.txt; the first failing step ends the call (no GPU work
 # after a fault, abort or time limit).  Steps:
-#   pytest:<file>[::expr]  python -u -m pytest <file> -m gpu -x -v (e.g. pytest:tests/test_rccl_gpu.py)
+#   pytest:<file>[::expr]  python -u -m pytest <file> -m gpu -x -v [-k "expr", commas read as spaces]
 #   pytest-all             every GPU test
 #   smoke                  __graft_entry__.smoke()
 #   bench[:args]           python bench.py <args with , as separator>  (bench:--force-comm,--steps,20)
@@ -33,7 +33,7 @@ for st in "$@"; do
   kind=${st%%:*}; rest=""; [ "$kind" != "$st" ] && rest=${st#*:}
   case $kind in
     pytest)
-      f=${rest%%::*}; k=""; [ "$f" != "$rest" ] && k=${rest#*::}
+      f=${rest%%::*}; k=""; [ "$f" != "$rest" ] && k=${rest#*::}; k=${k//,/ }
       n=$(basename "$f" .py)
       if [ -n "$k" ]; then
         run "pytest_$n" 900 python -u -m pytest "$f" -m gpu -x -v --timeout 240 --timeout-method thread -k "$k" || exit 1

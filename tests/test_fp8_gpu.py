@@ -136,7 +136,7 @@ FP8_CONV_SHAPES = [
     (2, 9, 9, 128, 128, 3, 3, 2, 1),      # 128-byte channel blocks, 64x128 tile
     (3, 7, 7, 256, 512, 1, 1, 1, 0),
     (4, 56, 56, 64, 256, 1, 1, 1, 0),     # 128x128 tile
-    (8, 28, 28, 128, 512, 1, 1, 1, 0),    # 256x256 tile
+    (8, 28, 28, 128, 512, 1, 1, 1, 0),    # M = 6272 <= 8192: 64x128 tile (256x256: test_tiles_gpu.py)
     (2, 16, 16, 512, 1024, 1, 1, 2, 0),
     (2, 14, 14, 256, 256, 3, 3, 1, 1),
 ]

@@ -1,0 +1,287 @@
+"""Every implicit-GEMM tile configuration the ResNet-50 bench runs, checked against fp32 PyTorch.
+
+``test_kernels_gpu.py`` covers the conv kernels on small shapes; the tile policy
+(``conv_nt_group_rows`` / ``plan_wgrad`` in ``csrc/kernels/conv_igemm.hip``) only selects the
+256x256 NT tile for GEMMs with >= 196 row tiles, which no small shape reaches.  Here each test
+asserts WHICH tile ran (``conv_nt_tile`` / ``conv_wgrad_plan`` introspection) and compares the
+kernel with an fp32 reference of the same op:
+
+* bf16 forward + BN partial statistics, plain dgrad, BN-fused dgrad in every ReLU-mask mode
+  (0 none, 1 z > 0, 2 recomputed from y, 3 bitmask) with and without the residual-gradient
+  addend, on the 256x256 / 128x128 / 256x64 / 64x128 tiles;
+* fp8 forward and dgrad on the 256x256 tile;
+* the whole ResNet-50 (224 px family at 112 px, batch 32) against the fp32 stock model with
+  identical weights;
+* the single-launch BN reductions (last-block handshake) against the two-launch path, and the
+  capped grid-stride BN passes against uncapped grids (each in a subprocess: both knobs are read
+  once per process).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_tutorials_amd.ops import reference as ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _operands(shape, dev, seed):
+    n, h, w, c, k, r, s, st, pd = shape
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    wt = (torch.randn(k, c, r, s, generator=g) / (c * r * s) ** 0.5).to(torch.bfloat16).float().to(dev)
+    wt = wt.contiguous(memory_format=torch.channels_last)
+    ho, wo = (h + 2 * pd - r) // st + 1, (w + 2 * pd - s) // st + 1
+    dy = torch.randn(n, ho, wo, k, generator=g).to(torch.bfloat16).to(dev)
+    return x, wt, dy
+
+
+# forward GEMM: M = N*Ho*Wo, Nout = K, K_gemm = R*S*C
+FWD_TILES = [
+    ((16, 56, 56, 128, 256, 1, 1, 1, 0), (256, 256)),   # layer1->2 style 1x1, 196 row tiles
+    ((64, 28, 28, 128, 256, 3, 3, 1, 1), (256, 256)),   # 3x3 on the wide tile
+    ((4, 56, 56, 64, 256, 1, 1, 1, 0), (128, 128)),
+    ((8, 32, 32, 64, 64, 3, 3, 1, 1), (256, 64)),
+    ((2, 14, 14, 256, 256, 3, 3, 1, 1), (64, 128)),
+]
+
+
+@pytest.mark.parametrize("shape,tile", FWD_TILES)
+def test_fwd_stats_per_tile(gpu, native_ext, shape, tile):
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, _ = _operands(shape, gpu, 1)
+    ho = (h + 2 * pd - r) // st + 1
+    M = n * ho * ho
+    assert tuple(C.conv_nt_tile(M, k, r * s * c * 2)) == tile
+    y, part = C.conv_fwd(x, C.pack_weight(wt, c), st, pd, True)
+    yr = ref.conv2d_nhwc(x, wt, st, pd)
+    assert _rel(y, yr) < 1e-2
+    assert part.shape[0] == (M + tile[0] - 1) // tile[0]  # one partial per workgroup row tile
+    stats = C.bn_finalize(part, M, torch.zeros(k, device=gpu), torch.ones(k, device=gpu),
+                          torch.ones(k, device=gpu), torch.zeros(k, device=gpu), 0.1, 1e-5)
+    mean_r, var_r = ref.bn_batch_stats(yr)
+    assert torch.allclose(stats[0], mean_r, atol=2e-3, rtol=1e-2)
+    assert torch.allclose(stats[1], torch.rsqrt(var_r + 1e-5), rtol=2e-2)
+
+
+# dgrad GEMM (per parity class): M = N*H*W / stride^2, Nout = C, K_gemm = R*S*K
+DGRAD_TILES = [
+    ((16, 56, 56, 256, 128, 1, 1, 1, 0), (256, 256)),
+    ((64, 28, 28, 256, 128, 3, 3, 1, 1), (256, 256)),
+    ((64, 56, 56, 256, 512, 1, 1, 2, 0), (256, 256)),   # stride-2 parity classes on the wide tile
+    ((4, 56, 56, 256, 64, 1, 1, 1, 0), (128, 128)),
+    ((8, 32, 32, 64, 64, 3, 3, 1, 1), (256, 64)),
+    ((2, 14, 14, 256, 256, 3, 3, 1, 1), (64, 128)),
+]
+
+
+def _bitmask(z):
+    bits = (z.reshape(-1, 8) > 0).to(torch.int32) << torch.arange(8, device=z.device, dtype=torch.int32)
+    return bits.sum(1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("shape,tile", DGRAD_TILES)
+def test_dgrad_and_bn_dgrad_per_tile(gpu, native_ext, shape, tile):
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, dy = _operands(shape, gpu, 2)
+    M = n * ((h + st - 1) // st) * ((w + st - 1) // st)  # parity class (0, 0)
+    assert tuple(C.conv_nt_tile(M, c, r * s * k * 2)) == tile
+    dxr = ref.conv2d_nhwc_dgrad(dy, wt, x.shape, st, pd)
+    dx = C.conv_dgrad(dy, wt, list(x.shape), st, pd)
+    assert _rel(dx, dxr) < 1e-2
+    # BN-fused epilogue: g = dx(+addend) * relu'(unit), partial sums vs the standalone reduction
+    g_ = torch.Generator().manual_seed(3)
+    y = torch.randn(n, h, w, c, generator=g_).to(torch.bfloat16).to(gpu)
+    mean = torch.randn(c, generator=g_).to(gpu) * 0.1
+    invstd = torch.rand(c, generator=g_).to(gpu) + 0.5
+    scale = torch.randn(c, generator=g_).to(gpu) * invstd
+    shift = torch.randn(c, generator=g_).to(gpu) * 0.1 - mean * scale
+    stats = torch.stack([mean, invstd, scale, shift]).contiguous()
+    z = torch.relu(torch.randn(n, h, w, c, generator=g_)).to(torch.bfloat16).to(gpu)
+    addend = torch.randn(n, h, w, c, generator=g_).to(torch.bfloat16).to(gpu)
+    for add in (None, addend):
+        base = C.conv_dgrad(dy, wt, list(x.shape), st, pd, add)
+        if add is not None:
+            assert _rel(base, dxr + add.float()) < 1e-2
+        for mask in (0, 1, 2, 3):
+            zin = z if mask == 1 else (_bitmask(z) if mask == 3 else None)
+            gk, sums = C.conv_dgrad_bn(dy, wt, list(x.shape), st, pd, add, y, zin, stats, mask)
+            if mask in (0, 1, 3):
+                on = torch.ones_like(z, dtype=torch.bool) if mask == 0 else (z.float() > 0)
+                assert torch.equal(gk, torch.where(on, base.float(), 0.0).to(torch.bfloat16)), (add is None, mask)
+            else:  # recomputed mask: fma ordering may flip exact-zero boundary cases
+                on = torch.addcmul(shift, y.float(), scale) > 0
+                agree = (gk.float() == torch.where(on, base.float(), 0.0)).float().mean().item()
+                assert agree > 0.999
+            sums_ref = C.bn_act_bwd_reduce(base, z, y, stats, 1 if mask == 3 else mask)
+            assert torch.allclose(sums, sums_ref, rtol=2e-3, atol=2e-3 * sums_ref.abs().max().item()), mask
+
+
+WGRAD_PLANS = [
+    ((16, 56, 56, 64, 256, 1, 1, 1, 0), 128),    # pointwise wgrad, 128-row tile
+    ((16, 56, 56, 64, 64, 3, 3, 1, 1), 64),      # Kout = 64: 64-row tile
+    ((16, 28, 28, 256, 512, 1, 1, 2, 0), 128),   # strided 1x1 (general loader)
+]
+
+
+@pytest.mark.parametrize("shape,bm", WGRAD_PLANS)
+@pytest.mark.parametrize("det", [False, True])
+def test_wgrad_per_plan(gpu, native_ext, shape, bm, det):
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, dy = _operands(shape, gpu, 4)
+    plan = C.conv_wgrad_plan(list(x.shape), list(wt.shape), st, pd, det)
+    assert plan["bm"] == bm and plan["splits"] > 1
+    dw = C.conv_wgrad(dy, x, list(wt.shape), st, pd, det)
+    assert _rel(dw, ref.conv2d_nhwc_wgrad(dy, x, wt.shape, st, pd)) < 1e-2
+
+
+def _deq(q, fmt):
+    return q.view(torch.float8_e4m3fn if fmt == 4 else torch.float8_e5m2).float()
+
+
+def test_fp8_fwd_and_dgrad_on_wide_tile(gpu, native_ext):
+    from pytorch_distributed_tutorials_amd.ops.fused import _packed_crsk8
+    C = native_ext
+    shape = (16, 56, 56, 256, 256, 1, 1, 1, 0)
+    n, h, w, c, k, r, s, st, pd = shape
+    assert tuple(C.conv_nt_tile(n * h * w, k, c)) == (256, 256)      # fwd: K_gemm bytes = C
+    assert tuple(C.conv_nt_tile(n * h * w, c, k)) == (256, 256)      # dgrad: K_gemm bytes = K
+    x, wt, dy = _operands(shape, gpu, 5)
+    x = torch.relu(x.float()).to(torch.bfloat16)
+    state = torch.zeros(C.fp8_state_floats(), device=gpu)
+    D = C.fp8_deq_offset()
+    C.quant_e4m3(x, state, 0)
+    xq = C.quant_e4m3(x, state, 1)
+    deq = state[D + 1:D + 2].clone()
+    wq, osc = C.pack_weight_fp8(wt, c, deq)
+    y, _ = C.conv_fwd_fp8(xq, wq, osc, st, pd, True)
+    xd = (_deq(xq, 4) * deq).to(gpu)
+    wd = (_deq(wq, 4).permute(0, 3, 1, 2) * (osc / deq)[:, None, None, None])
+    yr = ref.conv2d_nhwc(xd, wd.contiguous(memory_format=torch.channels_last), st, pd)
+    assert _rel(y, yr) < 1e-2
+    # dgrad: dy in e5m2 with a power-of-two scale, weights e4m3 per input channel
+    dy = (dy.float() * 1e-3).to(torch.bfloat16)
+    sc = 2.0 ** 14
+    dy8 = (dy.float() * sc).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+    wt8, wsc = _packed_crsk8(C, wt)
+    dx = C.conv_dgrad_fp8(dy8, wt8, wsc, torch.tensor([1.0 / sc], device=gpu), [n, h, w, c], st, pd)
+    dyd = (_deq(dy8, 5) / sc).to(torch.bfloat16)
+    wdd = (_deq(wt8, 4) * wsc[:, None, None, None]).permute(3, 0, 1, 2).contiguous(memory_format=torch.channels_last)
+    assert _rel(dx, ref.conv2d_nhwc_dgrad(dyd, wdd, (n, h, w, c), st, pd)) < 1e-2
+
+
+def _resnet50_grads(gpu, train):
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    torch.manual_seed(0)
+    mt = build_model("resnet50", num_classes=1000).to(gpu)
+    mb = copy.deepcopy(mt)                       # stock model under autocast bf16: the yardstick
+    mn = copy.deepcopy(mt).set_impl("native")
+    for m in (mt, mb, mn):
+        m.train(train)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(32, 3, 112, 112, generator=g).to(gpu)
+    y = torch.randint(0, 1000, (32,), generator=g).to(gpu)
+    lt = F.cross_entropy(mt(x), y)
+    lt.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lb = F.cross_entropy(mb(x), y)
+    lb.backward()
+    ln = ops.cross_entropy(mn(x), y)
+    ln.backward()
+    cat = lambda m: torch.cat([p.grad.float().flatten() for p in m.parameters()])  # noqa: E731
+    cos_n = F.cosine_similarity(cat(mn), cat(mt), dim=0).item()
+    cos_b = F.cosine_similarity(cat(mb), cat(mt), dim=0).item()
+    return lt.item(), lb.item(), ln.item(), cos_n, cos_b, mt, mn
+
+
+def test_resnet50_112px_matches_fp32_torch(gpu, native_ext):
+    """The whole native bf16 ResNet-50 vs the stock fp32 model with identical weights (batch 32,
+    112x112), with stock autocast-bf16 on the same weights as the noise yardstick.
+
+    Measured (scripts/diag_parity.py): with BatchNorm in TRAINING mode the gradient of a
+    random-init ResNet-50 is a near-cancellation -- bf16 rounding alone moves its direction to a
+    global cosine of ~0.16 against fp32 for stock autocast too (native ~0.14); in eval mode both
+    agree to > 0.998.  So: loss within 2 %, train-mode direction no worse than stock bf16 (minus
+    a margin), eval-mode direction > 0.99."""
+    lt, lb, ln, cos_n, cos_b, mt, mn = _resnet50_grads(gpu, train=True)
+    assert abs(ln - lt) < 2e-2 * abs(lt), (ln, lt)
+    assert cos_n > cos_b - 0.1, (cos_n, cos_b)
+    for (name, bt), (_, bn) in zip(mt.named_buffers(), mn.named_buffers()):
+        if bt.dtype == torch.int64:
+            assert torch.equal(bn, bt), name
+        else:  # running stats: per-tensor relative error (deep layers drift by bf16 noise)
+            assert _rel(bn, bt) < 3e-2, (name, _rel(bn, bt))
+    lt, lb, ln, cos_n, cos_b, _, _ = _resnet50_grads(gpu, train=False)
+    assert abs(ln - lt) < 1e-2 * abs(lt), (ln, lt)
+    assert cos_n > 0.99 and cos_n >= cos_b - 1e-3, (cos_n, cos_b)
+
+
+_BN_SCRIPT = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+from pytorch_distributed_tutorials_amd.ops import native
+C = native()
+dev = torch.device("cuda:0")
+g = torch.Generator().manual_seed(0)
+out = {}
+# forward finalize with many partitions (ResNet-50 layer1 grid: 3136 row groups x 64 channels)
+for (m, k, grows) in [(802816, 64, 256), (200704, 512, 256), (50176, 1024, 128)]:
+    ng = (m + grows - 1) // grows
+    y = torch.randn(ng, grows, k, generator=g).to(dev)
+    s = y.sum(1)
+    q = ((y - y.mean(1, keepdim=True)) ** 2).sum(1)
+    part = torch.stack([s, q], 1).contiguous()
+    rm, rv = torch.zeros(k, device=dev), torch.ones(k, device=dev)
+    st = C.bn_finalize(part, ng * grows, rm, rv, torch.ones(k, device=dev), torch.zeros(k, device=dev), 0.1, 1e-5)
+    out[f"fin{m}"] = [st.cpu().flatten().tolist(), rm.cpu().tolist(), rv.cpu().tolist()]
+# backward reduction and the capped-grid streaming passes (residual case > 32768 x 256 vectors)
+for shape in [(128, 56, 56, 256), (64, 28, 28, 512)]:
+    k = shape[-1]
+    dz = torch.randn(*shape, generator=g).to(torch.bfloat16).to(dev)
+    yy = torch.randn(*shape, generator=g).to(torch.bfloat16).to(dev)
+    res = torch.randn(*shape, generator=g).to(torch.bfloat16).to(dev)
+    stats = torch.stack([torch.randn(k, generator=g) * 0.1, torch.rand(k, generator=g) + 0.5,
+                         torch.rand(k, generator=g) + 0.5, torch.randn(k, generator=g) * 0.1]).to(dev).contiguous()
+    z, zm = C.bn_act_fwd_mask(yy, stats[2], stats[3], res)
+    sums = C.bn_act_bwd_reduce(dz, z, yy, stats, 1)
+    dy, dres = C.bn_act_bwd_apply(dz, z, yy, stats, torch.ones(k, device=dev), sums, 1, True, True)
+    key = "x".join(map(str, shape))
+    out["z" + key] = [float(z.float().sum()), float(z.float().abs().sum()), int(zm.int().sum())]
+    out["s" + key] = sums.cpu().flatten().tolist()
+    out["d" + key] = [float(dy.float().sum()), float(dy.float().abs().sum()), float(dres.float().abs().sum())]
+torch.cuda.synchronize()
+print(json.dumps(out))
+"""
+
+
+def _run_bn(env_extra):
+    env = dict(os.environ)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, "-c", _BN_SCRIPT, ROOT], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_bn_single_launch_reductions_match_two_launch_and_grid_caps(gpu):
+    base = _run_bn({})
+    two = _run_bn({"PDT_BN_LASTBLOCK": "0"})       # partials + separate finalize launch
+    small = _run_bn({"PDT_EW_BLOCKS": "256"})      # many grid-stride iterations per thread
+    assert base == two, "last-block handshake differs from the two-launch reduction"
+    assert base == small, "capped grid-stride passes differ from the default grids"
