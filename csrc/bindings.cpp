@@ -157,6 +157,17 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& wk, int64_t s
   return {y, part};
 }
 
+// Addend of a dgrad: the full [N,H,W,C] layout of dx (0), or a compact stride-2 map
+// [N, ceil(H/2), ceil(W/2), C] that contributes at even (h, w) only (2).
+static int addend_layout(const Tensor& addend, const Tensor& dx) {
+  check_bf16_nhwc(addend, "addend");
+  if (addend.sizes() == dx.sizes()) return 0;
+  TORCH_CHECK(addend.size(0) == dx.size(0) && addend.size(1) == (dx.size(1) + 1) / 2 &&
+              addend.size(2) == (dx.size(2) + 1) / 2 && addend.size(3) == dx.size(3),
+              "dgrad addend must have the shape of dx or be its stride-2 compact map");
+  return 2;
+}
+
 // wt: optional pre-packed bf16 [C][R][S][K] weights (flat-space dgrad mirror)
 Tensor packed_t_or_pack(const Tensor& w, const std::optional<Tensor>& wt) {
   if (wt.has_value() && wt->defined()) {
@@ -179,12 +190,12 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
   Tensor wt = packed_t_or_pack(w, wt_in);
   auto dx = at::empty({s.N, s.H, s.W, s.C}, dy.options());
   const uint16_t* ap = nullptr;
+  int asub = 0;
   if (addend.has_value() && addend->defined()) {
-    check_bf16_nhwc(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    asub = addend_layout(*addend, dx);
     ap = cbf(*addend);
   }
-  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, cur_stream(dy));
+  pdt::launch_conv_dgrad(cbf(dy), cbf(wt), bf(dx), ap, s, cur_stream(dy), nullptr, asub);
   return dx;
 }
 
@@ -220,9 +231,9 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
   }
   auto dx = at::empty({s.N, s.H, s.W, s.C}, y.options());
   const uint16_t* ap = nullptr;
+  int asub = 0;
   if (addend.has_value() && addend->defined()) {
-    check_bf16_nhwc(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    asub = addend_layout(*addend, dx);
     ap = cbf(*addend);
   }
   const int G = pdt::conv_dgrad_bn_groups(s, (int)dy_like.element_size());
@@ -232,7 +243,7 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
   auto sums = at::empty({2, s.C}, fopt);
   pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
   hipStream_t st = cur_stream(dy_like);
-  launch(s, bf(dx), ap, &bn, st);
+  launch(s, bf(dx), ap, &bn, st, asub);
   float* dg = nullptr;
   float* db = nullptr;
   if (dgamma.has_value() && dgamma->defined()) {
@@ -263,7 +274,9 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
   Tensor wt = packed_t_or_pack(w, wt_in);
   return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta,
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
-                           hipStream_t st) { pdt::launch_conv_dgrad(cbf(dy), cbf(wt), dx, ap, sh, st, bn); });
+                           hipStream_t st, int asub) {
+                         pdt::launch_conv_dgrad(cbf(dy), cbf(wt), dx, ap, sh, st, bn, asub);
+                       });
 }
 
 // fp8 dgrad operands: dy8 e5m2 NHWC [N,Ho,Wo,K], wt8 e4m3 [C,R,S,K] with per-C scale wscale,
@@ -291,13 +304,13 @@ Tensor conv_dgrad_fp8(const Tensor& dy8, const Tensor& wt8, const Tensor& wscale
   auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
   auto dx = at::empty({s.N, s.H, s.W, s.C}, dy8.options().dtype(at::kBFloat16));
   const uint16_t* ap = nullptr;
+  int asub = 0;
   if (addend.has_value() && addend->defined()) {
-    check_bf16_nhwc(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "dgrad addend shape mismatch");
+    asub = addend_layout(*addend, dx);
     ap = cbf(*addend);
   }
   pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(), wscale.data_ptr<float>(),
-                             ascale.data_ptr<float>(), bf(dx), ap, s, cur_stream(dy8));
+                             ascale.data_ptr<float>(), bf(dx), ap, s, cur_stream(dy8), nullptr, asub);
   return dx;
 }
 
@@ -312,10 +325,10 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fp8(const Tensor& dy8, const Tensor& wt
   auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
   return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta,
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
-                           hipStream_t st) {
+                           hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(),
                                                     wscale.data_ptr<float>(), ascale.data_ptr<float>(), dx,
-                                                    ap, sh, st, bn);
+                                                    ap, sh, st, bn, asub);
                        });
 }
 
@@ -468,8 +481,23 @@ Tensor bn_eval_params(const Tensor& rm, const Tensor& rv, const Tensor& gamma, c
   return out;
 }
 
+// optional BatchNorm of the residual (res_scale / res_shift: fp32 [K]); returns their pointers
+static std::pair<const float*, const float*> res_bn_args(const std::optional<Tensor>& res,
+                                                         const std::optional<Tensor>& rsc,
+                                                         const std::optional<Tensor>& rsh, int64_t K) {
+  const bool has = rsc.has_value() && rsc->defined();
+  TORCH_CHECK(has == (rsh.has_value() && rsh->defined()), "res_scale and res_shift go together");
+  if (!has) return {nullptr, nullptr};
+  TORCH_CHECK(res.has_value() && res->defined(), "a residual BatchNorm needs the residual");
+  for (const Tensor* t : {&*rsc, &*rsh})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == K,
+                "res_scale / res_shift must be contiguous fp32 [K] device tensors");
+  return {rsc->data_ptr<float>(), rsh->data_ptr<float>()};
+}
+
 Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
-                  const std::optional<Tensor>& res, bool relu) {
+                  const std::optional<Tensor>& res, bool relu, const std::optional<Tensor>& rsc,
+                  const std::optional<Tensor>& rsh) {
   check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(y.get_device());
   int K = y.size(3);
@@ -480,16 +508,19 @@ Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
     TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
     rp = cbf(*res);
   }
+  auto rbn = res_bn_args(res, rsc, rsh, K);
   auto z = at::empty_like(y);
   pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z), M,
-                         K, cur_stream(y));
+                         K, cur_stream(y), nullptr, rbn.first, rbn.second);
   return z;
 }
 
 // (z, zmask): bn_act_fwd with ReLU that also writes the 1-bit-per-element ReLU mask (uint8, one
 // byte per 8 channels) for a later BN-fused dgrad (mask mode 3)
 std::tuple<Tensor, Tensor> bn_act_fwd_mask(const Tensor& y, const Tensor& scale, const Tensor& shift,
-                                           const std::optional<Tensor>& res) {
+                                           const std::optional<Tensor>& res,
+                                           const std::optional<Tensor>& rsc,
+                                           const std::optional<Tensor>& rsh) {
   check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(y.get_device());
   int K = y.size(3);
@@ -500,10 +531,11 @@ std::tuple<Tensor, Tensor> bn_act_fwd_mask(const Tensor& y, const Tensor& scale,
     TORCH_CHECK(res->sizes() == y.sizes(), "residual shape mismatch");
     rp = cbf(*res);
   }
+  auto rbn = res_bn_args(res, rsc, rsh, K);
   auto z = at::empty_like(y);
   auto zm = at::empty({y.numel() / 8}, y.options().dtype(at::kByte));
   pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, true, bf(z), M, K,
-                         cur_stream(y), zm.data_ptr<uint8_t>());
+                         cur_stream(y), zm.data_ptr<uint8_t>(), rbn.first, rbn.second);
   return {z, zm};
 }
 
@@ -943,9 +975,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_finalize", checked("bn_finalize", &bn_finalize));
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
-        py::arg("residual"), py::arg("relu"));
+        py::arg("residual"), py::arg("relu"), py::arg("res_scale") = py::none(),
+        py::arg("res_shift") = py::none());
   m.def("bn_act_fwd_mask", checked("bn_act_fwd_mask", &bn_act_fwd_mask), py::arg("y"), py::arg("scale"),
-        py::arg("shift"), py::arg("residual"));
+        py::arg("shift"), py::arg("residual"), py::arg("res_scale") = py::none(),
+        py::arg("res_shift") = py::none());
   m.def("bn_act_bwd_reduce", checked("bn_act_bwd_reduce", &bn_act_bwd_reduce), py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply));

@@ -188,25 +188,39 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <bool RES, bool RELU, bool MASK = false>
+// RESBN: the residual is a raw (pre-BN) conv output with its own BatchNorm -- the projection
+// shortcut of a downsampling block.  It is normalised here and rounded to bf16 exactly as a
+// separate apply pass would have stored it, so the block output is bit-identical to the unfused
+// path while the normalised shortcut is never written or read back (2 x |shortcut| of HBM).
+template <bool RES, bool RELU, bool MASK = false, bool RESBN = false>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
                                                          const uint4* __restrict__ res,
                                                          uint4* __restrict__ z, int64_t nvec,
-                                                         int K8, uint8_t* __restrict__ zmask = nullptr) {
+                                                         int K8, uint8_t* __restrict__ zmask = nullptr,
+                                                         const float* __restrict__ rscale = nullptr,
+                                                         const float* __restrict__ rshift = nullptr) {
   // the grid stride is a multiple of K8 (ew_blocks), so a thread's 8-channel group and its
   // scale/shift are fixed over the loop (no 64-bit modulo and 4 coefficient loads per vector)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(v0 % K8) * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8(scale + c0, sc);
   load8(shift + c0, sh);
+  if constexpr (RESBN) {
+    load8(rscale + c0, rsc);
+    load8(rshift + c0, rsh);
+  }
   for (int64_t v = v0; v < nvec; v += stride) {
     f8 a = unpack8(y[v]);
     f8 r;
     if (RES) r = unpack8(res[v]);
+    if constexpr (RESBN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r.v[j] = bf2f(f2bf(fmaf(r.v[j], rsc[j], rsh[j])));
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = fmaf(a.v[j], sc[j], sh[j]);
@@ -253,13 +267,28 @@ static int ew_blocks(int64_t nvec, int K8, int cap_default = kEwCap) {
 
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
-                       hipStream_t st, uint8_t* zmask) {
+                       hipStream_t st, uint8_t* zmask, const float* rscale, const float* rshift) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
   dim3 g(ew_blocks(nvec, K8, res ? kEwCapResidual : kEwCap)), b(256);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto R = reinterpret_cast<const uint4*>(res);
   auto Z = reinterpret_cast<uint4*>(z);
+  if (rscale != nullptr) {  // residual = BN(raw shortcut conv output), normalised on the fly
+    if (!res || !rshift) throw std::runtime_error("bn_act_fwd: residual BN needs the residual and its shift");
+    if (zmask) {
+      if (!relu) throw std::runtime_error("bn_act_fwd: a ReLU mask needs relu");
+      hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+                         zmask, rscale, rshift);
+    } else if (relu) {
+      hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, false, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec,
+                         K8, nullptr, rscale, rshift);
+    } else {
+      hipLaunchKernelGGL((bn_act_fwd_kernel<true, false, false, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec,
+                         K8, nullptr, rscale, rshift);
+    }
+    return;
+  }
   if (zmask) {
     if (!relu) throw std::runtime_error("bn_act_fwd: a ReLU mask needs relu");
     if (res) hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8, zmask);

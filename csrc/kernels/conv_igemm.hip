@@ -133,6 +133,11 @@ struct NtArgs {
   const float* bn_stats;  // [4][Nout] mean, invstd, scale, shift
   float* bn_part;
   int bn_mask, bn_group0;
+  // addend layout: 0 = same NHWC layout as out; 2 = compact stride-2 map addend[n][h/2][w/2] that
+  // contributes only at even (h, w) -- the input gradient of a 1x1/s2 projection shortcut, which
+  // is zero at every odd position and is never materialised at full resolution
+  int add_sub, add_h, add_w;
+  uint32_t add_bytes;  // bytes of the addend tensor
 };
 
 // epilogue variants of the NT kernel
@@ -574,6 +579,7 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll 1
     for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
       uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
+      uint32_t aoff[IT];  // byte offset of the chunk in a compact (stride-2) addend, or OOB
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int qd = lane + (b0 + it) * 64;
@@ -581,23 +587,34 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
         const int m = wrow0 + r;
         const int col = wcol0 + c * 8;
         ooff[it] = OOB;
+        aoff[it] = OOB;
         if (m < P.M && col < P.Nout) {
           int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
-          if (!P.dense) {    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+          if (!P.dense || (HA && P.add_sub)) {
             uint32_t n = fdiv((uint32_t)m, P.div_ij);
             uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
             uint32_t ii = fdiv(rem, P.div_j);
             uint32_t jj = rem - ii * (uint32_t)P.Mj;
-            orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+            if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+              orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+            if (HA && P.add_sub) {
+              // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
+              // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
+              const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
+              const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
+              if (((hh | ww) & 1) == 0)
+                aoff[it] = (uint32_t)(((((int64_t)n * P.add_h + (hh >> 1)) * P.add_w + (ww >> 1)) * P.Nout + col) * 2);
+            }
           }
           ooff[it] = (uint32_t)((orow * P.Nout + col) * 2);
+          if (HA && !P.add_sub) aoff[it] = ooff[it];
         }
       }
       v4i av[IT], yv[IT], zv[IT];
       if constexpr (HA) {
-        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.o_bytes);
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.add_bytes);
 #pragma unroll
-        for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, ooff[it]);
+        for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, aoff[it]);
       }
       if constexpr (EPI == EPI_BNB) {
         const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
@@ -1250,7 +1267,8 @@ int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes) {
 template <int OP>
 static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale, const float* ascale,
                             uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
-                            const BnBwdFuse* bn) {
+                            const BnBwdFuse* bn, int addend_sub) {
+  if (addend_sub != 0 && addend_sub != 2) throw std::runtime_error("conv_dgrad: addend_sub must be 0 or 2");
   constexpr int EB = OP == OP_BF16 ? 2 : 1;
   if (s.K % (128 / EB) != 0)
     throw std::runtime_error("conv_dgrad: output channels must fill 128-byte rows (64 bf16 / 128 fp8)");
@@ -1261,6 +1279,10 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       NtArgs a{};
       a.a = reinterpret_cast<const uint16_t*>(dy); a.b = reinterpret_cast<const uint16_t*>(wt);
       a.out = dx; a.addend = addend; a.part = nullptr; a.oscale = oscale; a.ascale = ascale;
+      a.add_sub = addend ? addend_sub : 0;
+      a.add_h = addend_sub ? (s.H + 1) / 2 : s.H;
+      a.add_w = addend_sub ? (s.W + 1) / 2 : s.W;
+      a.add_bytes = (uint32_t)((int64_t)s.N * a.add_h * a.add_w * s.C * 2);
       a.a_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * EB);
       a.b_bytes = (uint32_t)((int64_t)s.C * s.R * s.S * s.K * EB);
       a.o_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
@@ -1295,14 +1317,14 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
 }
 
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn) {
-  conv_dgrad_impl<OP_BF16>(dy, wt, nullptr, nullptr, dx, addend, s, st, bn);
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn, int addend_sub) {
+  conv_dgrad_impl<OP_BF16>(dy, wt, nullptr, nullptr, dx, addend, s, st, bn, addend_sub);
 }
 
 void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,
                            uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
-                           const BnBwdFuse* bn) {
-  conv_dgrad_impl<OP_F8_E5M2>(dy, wt, oscale, ascale, dx, addend, s, st, bn);
+                           const BnBwdFuse* bn, int addend_sub) {
+  conv_dgrad_impl<OP_F8_E5M2>(dy, wt, oscale, ascale, dx, addend, s, st, bn, addend_sub);
 }
 
 // ------------------------------------------------------------------- wgrad

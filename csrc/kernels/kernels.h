@@ -70,8 +70,11 @@ struct BnBwdFuse {
   int mask;
 };
 int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes = 2);
+// addend_sub = 2: addend is a compact [N, ceil(H/2), ceil(W/2), C] map added at even (h, w) only
+// (the input gradient of a 1x1/s2 projection shortcut, computed as a dense 1x1 dgrad)
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr);
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr,
+                       int addend_sub = 0);
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
@@ -94,9 +97,12 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
                            float eps, int K, float* out, hipStream_t st);
 // z = act(y*scale + shift (+res)); zmask (optional, with relu): one byte per 8 channels, bit q =
 // z[8i + q] > 0 -- the ReLU mask a later backward reads instead of z (1/16 of the bytes)
+// rscale/rshift (optional): the residual is a raw conv output to normalise as bf16(res*rscale +
+// rshift) first -- a downsampling block's projection shortcut, whose BN apply is fused here
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
-                       hipStream_t st, uint8_t* zmask = nullptr);
+                       hipStream_t st, uint8_t* zmask = nullptr, const float* rscale = nullptr,
+                       const float* rshift = nullptr);
 // Backward BN.  stats = bn_finalize output [4][K] (mean, invstd, scale, shift).  mask: 0 = no
 // ReLU, 1 = ReLU mask from z (> 0), 2 = ReLU mask recomputed from y (y*scale + shift > 0).
 // sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * mask; ws >= bn_bwd_ws_floats(M, K)
@@ -199,7 +205,7 @@ void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale
 // activation (dy) dequant factor ascale[0]; otherwise as launch_conv_dgrad
 void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,
                            uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
-                           const BnBwdFuse* bn = nullptr);
+                           const BnBwdFuse* bn = nullptr, int addend_sub = 0);
 // bn_act_bwd_apply that also writes dy8 = e5m2(bf16(dy) * s_t) (delayed scaling, fp8 state contract)
 void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                                 const float* stats, const float* gamma, const float* sums, int mask,

@@ -35,6 +35,8 @@ _ZMASK = os.environ.get("PDT_ZMASK", "1") != "0"  # 1-bit ReLU masks for the han
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
 _FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
 _FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input-gradient GEMMs
+_FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
+_COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
 
 
 def set_fp8(on: bool) -> None:
@@ -572,7 +574,30 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
               x8=None, q8=None, want_mask=False):
     """conv -> BN -> (+residual) -> (ReLU) -> (z, y, stats, z8, zmask).  x8 = (e4m3 copy of x, its
     dequant factor): fp8 conv; q8 = _Q8State: also emit the e4m3 copy z8 of the output;
-    want_mask (with relu): also the 1-bit ReLU mask zmask a later BN-fused dgrad reads instead of z."""
+    want_mask (with relu): also the 1-bit ReLU mask zmask a later BN-fused dgrad reads instead of z.
+    ``residual`` is an activation, or ``(y_short, stats_short)``: a projection shortcut's raw conv
+    output and its BN statistics, normalised inside this unit's apply pass (never materialised)."""
+    y, stats = _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, momentum, eps, x8)
+    k = w.shape[0]
+    rsc = rsh = None
+    if isinstance(residual, tuple):
+        residual, rst = residual
+        rsc, rsh = rst[2], rst[3]
+    want_mask = want_mask and relu
+    if q8 is not None and k % 16 == 0:
+        assert rsc is None, "fp8 apply takes a materialised residual"
+        slot = q8.next_slot()
+        z, zq, zm = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot, want_mask)
+        return z, y, stats, (zq, q8.deq(slot)), (zm if want_mask else None)
+    if want_mask:
+        z, zm = C.bn_act_fwd_mask(y, stats[2], stats[3], residual, rsc, rsh)
+        return z, y, stats, None, zm
+    z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu, rsc, rsh)
+    return z, y, stats, None, None
+
+
+def _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, momentum, eps, x8=None):
+    """conv -> BN statistics (finalize, running-stat update): (y, stats[4, K])."""
     k, _, r, s = w.shape
     n, h, wd, cx = x.shape
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
@@ -593,16 +618,7 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
         stats = C.bn_finalize(part, count, rm, rv, gamma, beta, float(momentum), float(eps))
     else:
         stats = C.bn_eval_params(rm, rv, gamma, beta, float(eps))
-    want_mask = want_mask and relu
-    if q8 is not None and k % 16 == 0:
-        slot = q8.next_slot()
-        z, zq, zm = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot, want_mask)
-        return z, y, stats, (zq, q8.deq(slot)), (zm if want_mask else None)
-    if want_mask:
-        z, zm = C.bn_act_fwd_mask(y, stats[2], stats[3], residual)
-        return z, y, stats, None, zm
-    z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu)
-    return z, y, stats, None, None
+    return y, stats
 
 
 class _BnHandoff:
@@ -645,7 +661,13 @@ class _ResidualBlock(torch.autograd.Function):
         if ds_cfg is not None:
             w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
             st, pd, tr, mo, ep = ds_cfg
-            res, y_ds, st_ds, _, _ = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None, x8)
+            if q8s is None and _FUSE_RES_BN:
+                # projection shortcut: conv + statistics only; its BN apply runs inside the block
+                # tail's apply pass (bn_act_fwd RESBN), so the normalised shortcut is never stored
+                y_ds, st_ds = _unit_conv_stats(C, x, w, g, b, rm, rv, st, pd, tr, mo, ep, x8)
+                res = (y_ds, st_ds)
+            else:
+                res, y_ds, st_ds, _, _ = _unit_fwd(C, x, w, g, b, rm, rv, st, pd, False, tr, mo, ep, None, x8)
         else:
             res = x
         h, h8 = x, x8
@@ -823,7 +845,15 @@ class _ResidualBlock(torch.autograd.Function):
                     dy_ds, _, d8_ds = apply(5 * nch, g_short, g_short, y_ds, st_ds, sums_ds, 0, tr2, False,
                                             ctx.needs_input_grad[0])
                     wgrad(5 * nch, dy_ds, x, st2, pd2)
-                    addend = dgrad(dy_ds, d8_ds, wds, list(x.shape), st2, pd2, None)
+                    if st2 == 2 and pd2 == 0 and wds.shape[2] == 1 and wds.shape[3] == 1 and _COMPACT_ADDEND:
+                        # 1x1/s2 shortcut: its input gradient is zero at every odd (h, w), so it is
+                        # computed as a dense 1x1 dgrad on the stride-2 grid and the first conv's
+                        # dgrad epilogue adds it at even positions only (no full-resolution tensor,
+                        # no all-zero parity-class launches)
+                        n_, h_, w_, c_ = x.shape
+                        addend = dgrad(dy_ds, d8_ds, wds, [n_, (h_ + 1) // 2, (w_ + 1) // 2, c_], 1, 0, None)
+                    else:
+                        addend = dgrad(dy_ds, d8_ds, wds, list(x.shape), st2, pd2, None)
                 else:
                     addend = g_short
                 if not ctx.needs_input_grad[0]:

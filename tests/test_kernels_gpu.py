@@ -330,7 +330,8 @@ def test_resnet18_native_matches_torch(gpu, native_ext):
         assert torch.allclose(bn.float().cpu(), bt.float(), atol=5e-2, rtol=5e-2), name
 
 
-@pytest.mark.parametrize("arch,idx", [("resnet50", (1, 0)), ("resnet50", (1, 1)), ("resnet18", (2, 0))])
+@pytest.mark.parametrize("arch,idx", [("resnet50", (1, 0)), ("resnet50", (1, 1)), ("resnet50", (2, 0)),
+                                      ("resnet18", (2, 0))])
 def test_residual_block_matches_unit_path(gpu, native_ext, arch, idx):
     """The fused block autograd node == the per-unit conv_bn composition (same kernels)."""
     import copy
@@ -663,3 +664,49 @@ def test_trainer_graph_matches_eager(gpu, native_ext, tmp_path):
     assert sds[0].keys() == sds[1].keys()
     for k in sds[0]:
         assert torch.equal(sds[0][k], sds[1][k]), k
+
+
+@pytest.mark.parametrize("mask", [False, True])
+def test_bn_act_fwd_residual_bn_matches_materialised(gpu, native_ext, mask):
+    """Projection-shortcut BN applied inside the block-tail apply == applying it in its own pass
+    first (bit for bit: the fused kernel rounds the normalised shortcut to bf16 the same way)."""
+    C = native_ext
+    g = torch.Generator().manual_seed(21)
+    y = torch.randn(8, 14, 14, 256, generator=g).to(torch.bfloat16).to(gpu)
+    r = torch.randn(8, 14, 14, 256, generator=g).to(torch.bfloat16).to(gpu)
+    sc, sh = (torch.rand(256, generator=g) + 0.5).to(gpu), torch.randn(256, generator=g).to(gpu)
+    rsc, rsh = (torch.rand(256, generator=g) * 2 - 1).to(gpu), torch.randn(256, generator=g).to(gpu)
+    res = C.bn_act_fwd(r, rsc, rsh, None, False)
+    if mask:
+        z0, m0 = C.bn_act_fwd_mask(y, sc, sh, res)
+        z1, m1 = C.bn_act_fwd_mask(y, sc, sh, r, rsc, rsh)
+        assert torch.equal(m0, m1)
+    else:
+        z0 = C.bn_act_fwd(y, sc, sh, res, True)
+        z1 = C.bn_act_fwd(y, sc, sh, r, True, rsc, rsh)
+    assert torch.equal(z0, z1)
+
+
+@pytest.mark.parametrize("cfg", [(2, 28, 28, 256, 128, 1, 1, 1, 0),    # bottleneck conv1 (dense dgrad)
+                                 (2, 28, 28, 128, 128, 3, 3, 2, 1),    # BasicBlock conv1 (parity classes)
+                                 (2, 13, 13, 64, 64, 3, 3, 2, 1)])     # odd extent
+def test_compact_stride2_addend(gpu, native_ext, cfg):
+    """A stride-2 shortcut gradient passed as a compact [N, ceil(H/2), ceil(W/2), C] map == the same
+    values zero-interleaved at full resolution, for plain and BN-fused dgrad."""
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = cfg
+    g = torch.Generator().manual_seed(22)
+    ho, wo = (h + 2 * pd - r) // st + 1, (w + 2 * pd - s) // st + 1
+    dy = torch.randn(n, ho, wo, k, generator=g).to(torch.bfloat16).to(gpu)
+    wt = (torch.randn(k, c, r, s, generator=g) * 0.05).to(gpu).contiguous(memory_format=torch.channels_last)
+    comp = torch.randn(n, (h + 1) // 2, (w + 1) // 2, c, generator=g).to(torch.bfloat16).to(gpu)
+    full = torch.zeros(n, h, w, c, dtype=torch.bfloat16, device=gpu)
+    full[:, ::2, ::2, :] = comp
+    assert torch.equal(C.conv_dgrad(dy, wt, [n, h, w, c], st, pd, comp),
+                       C.conv_dgrad(dy, wt, [n, h, w, c], st, pd, full))
+    y = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(gpu)
+    stats = torch.stack([torch.zeros(c), torch.ones(c), torch.rand(c, generator=g) + 0.5,
+                         torch.randn(c, generator=g) * 0.1]).to(gpu).contiguous()
+    a = C.conv_dgrad_bn(dy, wt, [n, h, w, c], st, pd, comp, y, None, stats, 2)
+    b = C.conv_dgrad_bn(dy, wt, [n, h, w, c], st, pd, full, y, None, stats, 2)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
