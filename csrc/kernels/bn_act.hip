@@ -877,7 +877,14 @@ void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* 
                      reinterpret_cast<uint2*>(idx), (uint32_t)total, H, W, log2_exact(C8), Ho, Wo);
 }
 
-size_t pool_bn_bwd_ws_floats(int64_t M, int K) { return bn_bwd_ws_floats(M, K); }
+// The stem's fused pool/BN reduction gathers each 2x2 quad's pooled gradient (dependent loads)
+// before its y loads, so it needs more blocks in flight than the plain reduction to reach HBM
+// rate: up to 4096 (16 per CU requested; ~2.1 TB/s with the plain reduction's 1024).
+constexpr int POOL_RED_BLOCKS = 4096;
+static int pool_red_blocks(int NQ) { return std::max(1, std::min(POOL_RED_BLOCKS, NQ / 8)); }
+size_t pool_bn_bwd_ws_floats(int64_t M, int K) {
+  return std::max(bn_bwd_ws_floats(M, K), (size_t)POOL_RED_BLOCKS * 2 * K);
+}
 
 void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
                                const float* stats, int N, int H, int W, int K, int Ho, int Wo,
@@ -887,7 +894,7 @@ void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const 
   const int64_t M = (int64_t)N * H * W;
   if (M * K8 >= (int64_t)1 << 31) throw std::runtime_error("pool_bn_bwd_reduce: tensor too large");
   const int NQ = N * Ho * Wo;
-  const int nb = std::min(red_blocks(M, K), std::max(1, NQ / 8));  // <= bn_bwd_ws_floats(M, K) rows
+  const int nb = pool_red_blocks(NQ);  // <= pool_bn_bwd_ws_floats(M, K) rows
   hipLaunchKernelGGL(pool_bn_bwd_reduce_kernel, dim3(nb), dim3(256), 256 * 16 * sizeof(float), st,
                      reinterpret_cast<const uint4*>(dpool), reinterpret_cast<const uint2*>(idx),
                      reinterpret_cast<const uint4*>(y), stats, NQ, K8, H, W, Ho, Wo, ws);

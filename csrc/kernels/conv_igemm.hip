@@ -1361,7 +1361,7 @@ static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   p.tiles = ((s.K + p.bmg - 1) / p.bmg) * ((ncols + p.bng - 1) / p.bng);
   const int64_t mred = (int64_t)s.N * s.Ho * s.Wo;
   p.nsteps = (int)((mred + 63) / 64);
-  int target = p.bmg == 256 ? 512 : 1024;  // ~4 4-wave (2 8-wave) blocks per CU
+  int target = p.bmg == 256 ? 512 : (p.tiles <= 4 ? 2048 : 1024);  // ~4 4-wave (2 8-wave) blocks per CU
   int splits = (target + p.tiles - 1) / p.tiles;
   splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
   // bound the reduction traffic: atomics/slabs move splits * |dW| * 4 bytes
@@ -1377,7 +1377,9 @@ static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   }
   const int64_t cap_bytes = (deterministic ? cap_slab : cap_atomic) << 20;
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, cap_bytes / dw_bytes));
-  splits = std::max(1, std::min(splits, 256));
+  // atomic split-K: up to 1024 slices (the stem's 2-tile, 50k-step wgrad runs last in backward,
+  // on the critical path: 256 slices left it at 2 blocks per CU); slabs keep 256
+  splits = std::max(1, std::min(splits, deterministic ? 256 : 1024));
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
   return p;
