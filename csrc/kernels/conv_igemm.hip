@@ -138,6 +138,13 @@ struct NtArgs {
   // is zero at every odd position and is never materialised at full resolution
   int add_sub, add_h, add_w;
   uint32_t add_bytes;  // bytes of the addend tensor
+  // HALO (3x3, stride 1, same-size output): the A tile of a channel block is staged ONCE as the
+  // halo of the tile's image rows -- halo_rows x (WA + 2) pixels of 128 B -- and the 9 taps read
+  // shifted views of it, instead of 9 separate 256-row A tiles (9x the L2->LDS traffic)
+  int halo_rows, halo_nbuf, n_cb;
+  uint32_t halo_bytes;
+  FastDiv div_hw2;  // halo pixel -> halo row (divide by WA + 2)
+  FastDiv div_ha;   // global image row -> image (divide by HA)
 };
 
 // epilogue variants of the NT kernel
@@ -205,8 +212,9 @@ __device__ __forceinline__ void wait_steps(int younger) {
 // MFMA operands are swapped (A = weights, B = pixels) so each lane's 4 accumulator registers are
 // 4 consecutive output channels of one pixel: the epilogue packs them into one 8-byte LDS write
 // and the BN statistics reduce over the 16 pixel-lanes with DPP-friendly xor shuffles.
-template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16>
-__global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) {
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool HALO = false>
+__global__ void __launch_bounds__(WM * WN * 64, (HALO && WM * WN == 4) ? 2 : 1) igemm_nt_kernel(const NtArgs P) {
+  static_assert(!HALO || (C64 && OP == OP_BF16), "halo staging: bf16, 64-channel blocks");
   using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   constexpr int EB = OP == OP_BF16 ? 2 : 1;  // bytes per element
@@ -381,6 +389,112 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (HALO) {
+    // ------------------------------------------------ halo main loop (3x3 / s1 / same size)
+    // LDS: [halo buffers][B stage 0][B stage 1][zero row].  K-steps run channel block (outer) x
+    // tap (inner); B moves one [BN][64] tile per step (2 buffers), the halo of the next channel
+    // block is fetched while the current one's 9 taps compute (2 buffers) or after them (1).
+    const int WP = P.WA + 2;                        // halo row pitch in pixels (zero pad columns)
+    const int g_first = (int)fdiv((uint32_t)m0, P.div_j);  // first global image row (n*HA + h)
+    const int NH = P.M / P.WA;                      // global rows of the activation
+    char* hbase = smem;
+    char* bbase = smem + P.halo_nbuf * P.halo_bytes;
+    char* zrow = bbase + 2 * BN * 128;
+    if (t < 8) *reinterpret_cast<v4i*>(zrow + t * 16) = v4i{0, 0, 0, 0};
+    // this lane's fragment pixels: halo pixel of the centre tap + which vertical taps stay inside
+    // its image (a halo row above / below can belong to the neighbouring image: read zeros)
+    int hp0[TM];
+    uint32_t vrow[TM];  // bit 0: row above inside the image, bit 1: row below, bit 2: pixel < M
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int p = m0 + wm * TM * 16 + i * 16 + fr;
+      if (p < P.M) {
+        const uint32_t g = fdiv((uint32_t)p, P.div_j);
+        const int w = p - (int)g * P.WA;
+        const int h = (int)(g - fdiv(g, P.div_ha) * (uint32_t)P.HA);
+        hp0[i] = ((int)g - g_first + 1) * WP + w + 1;
+        vrow[i] = 4u | (h > 0 ? 1u : 0u) | (h + 1 < P.HA ? 2u : 0u);
+      } else {
+        hp0[i] = WP + 1;
+        vrow[i] = 0u;  // rows past the GEMM: every tap reads zeros
+      }
+    }
+    const int hpix = P.halo_rows * WP;
+    const int nq = (hpix + 7) / 8;  // 1-KiB DMA instructions per halo
+    auto issue_halo = [&](int cb, int hb) {
+      char* dst = hbase + hb * P.halo_bytes;
+      for (int q = wid; q < nq; q += CFG::WAVES) {
+        const int hp = q * 8 + lr;
+        const int hr = (int)fdiv((uint32_t)hp, P.div_hw2);
+        const int col = hp - hr * WP - 1;
+        const int g = g_first - 1 + hr;
+        const bool ok = hp < hpix && g >= 0 && g < NH && (unsigned)col < (unsigned)P.WA;
+        const int ch = lj ^ ((hp >> 1) & 7);
+        const uint32_t off = ok ? (uint32_t)((((int64_t)g * P.WA + col) * P.CA + cb * 64 + ch * 8) * 2) : OOB;
+        glds16(ra, dst + q * 1024, off);
+      }
+    };
+    auto issue_b = [&](int ti, int tj, int cb, int bb) {
+      char* Bs = bbase + bb * BN * 128;
+      const int tbo = ((P.tr0 + ti * P.tstep) * P.S + (P.ts0 + tj * P.tstep)) * P.CA + cb * 64;
+#pragma unroll
+      for (int i = 0; i < B_PW; ++i) {
+        const uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * 2 + b_c[i] * 16) : OOB;
+        glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
+      }
+    };
+    const int ntap = P.tnr * P.tns;
+    const int nk_h = ntap * P.n_cb;
+    issue_halo(0, 0);
+    issue_b(0, 0, 0, 0);
+    wait_vm<0>();
+    __syncthreads();  // zero row + first tiles visible
+    int ti = 0, tj = 0, cb = 0;      // K-step kt = cb * ntap + ti * tns + tj
+    int ni = 0, nj = 0, ncb = 0;     // the next step's (tap row, tap col, channel block)
+    for (int kt = 0; kt < nk_h; ++kt) {
+      // next step's coordinates
+      ni = ti; nj = tj + 1; ncb = cb;
+      if (nj == P.tns) { nj = 0; if (++ni == P.tnr) { ni = 0; ++ncb; } }
+      const bool more = kt + 1 < nk_h;
+      const bool new_cb = more && ncb != cb;
+      if (more) {
+        issue_b(ni, nj, ncb, (kt + 1) & 1);
+        if (new_cb && P.halo_nbuf == 2) issue_halo(ncb, ncb & 1);
+      }
+      const int dr = P.aoff_h + P.dr0 + ti * P.dstep;  // -1, 0 or +1
+      const int ds = P.aoff_w + P.ds0 + tj * P.dstep;
+      const int dtap = dr * WP + ds;
+      const uint32_t need = 4u | (dr < 0 ? 1u : (dr > 0 ? 2u : 0u));
+      const char* Hs = hbase + (P.halo_nbuf == 2 ? (cb & 1) : 0) * P.halo_bytes;
+      const char* Bs = bbase + (kt & 1) * BN * 128;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kc = ks * 4 + fq;
+        v4i af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int hp = hp0[i] + dtap;
+          const bool ok = (vrow[i] & need) == need;
+          const char* src = ok ? Hs + hp * 128 + ((kc ^ ((hp >> 1) & 7)) << 4) : zrow + kc * 16;
+          af[i] = *reinterpret_cast<const v4i*>(src);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(wn * TN * 16 + j * 16 + fr, kc));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      }
+      if (new_cb && P.halo_nbuf == 1) {  // single halo buffer: refill after every wave read it
+        lds_barrier();
+        issue_halo(ncb, 0);
+      }
+      wait_vm<0>();
+      lds_barrier();
+      ti = ni; tj = nj; cb = ncb;
+    }
+  } else {
   constexpr int LPS = A_PW + B_PW;
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
@@ -435,6 +549,7 @@ __global__ void __launch_bounds__(WM * WN * 64) igemm_nt_kernel(const NtArgs P) 
     cur = cur + 1 == STAGES ? 0 : cur + 1;
     nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
   }
+  }  // !HALO
 
   // --------------------------------------------------------------- epilogue
   // lane (fq, fr), register e of acc[i][j]: pixel i*16 + fr, channel j*16 + fq*4 + e
@@ -1096,6 +1211,58 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
   check_launch("igemm_nt");
 }
 
+template <int WM, int WN, int TM, int TN, int EPI>
+static void run_nt_halo(const NtArgs& a, hipStream_t st) {
+  using CFG = NtCfg<WM, WN, TM, TN, 2>;
+  const int ntm = (a.M + CFG::BM - 1) / CFG::BM;
+  const int ntn = (a.Nout + CFG::BN - 1) / CFG::BN;
+  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, 2, true, EPI, OP_BF16, true>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const int smem = std::max((int)(a.halo_nbuf * a.halo_bytes) + 2 * CFG::BN * 128 + 128, CFG::EPI_BYTES);
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), smem, st, a);
+  check_launch("igemm_nt_halo");
+}
+
+// Halo staging for 3x3 / stride 1 / pad 1 convolutions (fwd and dgrad): fills the halo fields of
+// `a` for the tile the dispatcher will pick and returns false where it does not apply or does
+// not fit in LDS.  PDT_HALO=0 disables it (A/B knob).
+static bool halo_mode() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_HALO");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
+  // Measured on MI355X (r2p/r2q, bench_conv.py, batch 256): halo staging pays where one channel
+  // block covers the whole reduction (C = 64, ResNet layer1: fwd 114 -> 103 us, dgrad 111 -> 98,
+  // BN-fused dgrad 140 -> 130); with several channel blocks the halo reload per block stalls
+  // (128x28x28: 86 -> 93 us, 512x7x7: 75 -> 88), so those keep the per-tap A tiles.
+  if (!halo_mode() || R != 3 || S != 3 || tap_stride != 1 || pad != 1 || a.CA != 64 || !a.dense) return false;
+  int bm = 0, bn = 0;
+  conv_nt_tile(a.M, a.Nout, a.Kg * 2, &bm, &bn);
+  const int WP = a.WA + 2;
+  a.halo_rows = (a.WA + bm - 2) / a.WA + 3;
+  const int hpix = a.halo_rows * WP;
+  a.halo_bytes = (uint32_t)((hpix + 7) / 8) * 1024;
+  a.n_cb = a.CA / 64;
+  const int bstage = 2 * bn * 128 + 128;
+  const bool wide = bm == 256 && bn == 256;  // 8-wave tile: one block per CU regardless
+  const int cap2 = wide ? 160 * 1024 : 80 * 1024;
+  if (a.n_cb > 1 && 2 * (int)a.halo_bytes + bstage <= cap2) a.halo_nbuf = 2;
+  else if ((int)a.halo_bytes + bstage <= 160 * 1024) a.halo_nbuf = 1;
+  else return false;
+  a.div_hw2 = make_fastdiv((uint32_t)WP);
+  a.div_ha = make_fastdiv((uint32_t)a.HA);
+  return true;
+}
+
 // Pipeline depth per NT tile (256x64, 64x128, 128x128); PDT_NT_STAGES="a,b,c" overrides.
 static int nt_stages(int which) {
   static int v[3] = {-1, -1, -1};
@@ -1156,6 +1323,15 @@ void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn) {
 template <bool C64, int EPI, int OP = OP_BF16>
 static void dispatch_nt(const NtArgs& a, hipStream_t st) {
   const int rows = conv_nt_group_rows(a.M, a.Nout, a.Kg * (OP == OP_BF16 ? 2 : 1));
+  if constexpr (C64 && OP == OP_BF16) {
+    if (a.halo_rows > 0) {
+      if (a.Nout <= 64) run_nt_halo<4, 1, 4, 4, EPI>(a, st);
+      else if (rows == 64) run_nt_halo<2, 2, 2, 4, EPI>(a, st);
+      else if (rows == 256) run_nt_halo<4, 2, 4, 8, EPI>(a, st);
+      else run_nt_halo<2, 2, 4, 4, EPI>(a, st);
+      return;
+    }
+  }
   if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
     if (a.Nout <= 64) run_nt<4, 1, 4, 4, 2, C64, EPI, OP>(a, st);
     else if (rows == 64) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
@@ -1204,6 +1380,7 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
   a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   bool c64 = (s.C % 64) == 0 && s.R * s.S <= 32;  // C64 loader: tap validity bitmask per row
+  if (c64 && s.sw() == s.stride && s.Ho == s.H && s.Wo == s.W) setup_halo(a, s.R, s.S, s.stride, s.pad);
   if (!c64 && s.C == 8 && 8 % s.S == 0) {
     a.c8 = 1;
     a.c8_rows = 8 / s.S;
@@ -1302,6 +1479,7 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       a.tnr = r0 < s.R ? (s.R - r0 + str - 1) / str : 0;
       a.tns = s0 < s.S ? (s.S - s0 + str - 1) / str : 0;
       a.ntaps = a.tnr * a.tns;  // 0 -> kernel writes zeros for this class
+      if (OP == OP_BF16 && str == 1 && s.H == s.Ho && s.W == s.Wo) setup_halo(a, s.R, s.S, 1, s.pad);
       if (a.ntaps > 32) throw std::runtime_error("conv_dgrad: more than 32 taps per parity class");
       a.tr0 = r0; a.ts0 = s0; a.tstep = str;
       a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;

@@ -20,8 +20,10 @@ cd "$R" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
 O="$R/gpurun_out"; mkdir -p "$O"
 npmc=0
-run() {  # run NAME SECONDS cmd...
-  local name=$1 secs=$2; shift 2
+nstep=0
+run() {  # run NAME SECONDS cmd...  (logs: TAG_<NN>_<name>.log, NN = step number)
+  nstep=$((nstep+1))
+  local name=$(printf "%02d_%s" $nstep "$1") secs=$2; shift 2
   echo "[$(date +%T)] $name: $*" | tee -a "$O/${TAG}_status.txt"
   timeout -k 10 "$secs" "$@" > "$O/${TAG}_${name}.log" 2>&1
   local rc=$?
