@@ -755,13 +755,103 @@ Tensor avgpool_fwd(const Tensor& x) {
   return y;
 }
 
+// dy: fp32 [N, C], or [splits, N, C] split-K partials of the fc dgrad (summed here, in order)
 Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   check_cuda(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.is_contiguous() && (dy.dim() == 2 || dy.dim() == 3),
+              "avgpool_bwd: dy must be contiguous fp32 [N, C] or [splits, N, C]");
   c10::hip::HIPGuard g(dy.get_device());
-  int N = dy.size(0), C = dy.size(1);
+  const int splits = dy.dim() == 3 ? (int)dy.size(0) : 1;
+  int N = dy.size(dy.dim() - 2), C = dy.size(dy.dim() - 1);
   auto dx = at::empty({N, H, W, C}, dy.options().dtype(at::kBFloat16));
-  pdt::launch_avgpool_bwd(dy.data_ptr<float>(), bf(dx), N, (int)(H * W), C, cur_stream(dy));
+  pdt::launch_avgpool_bwd(dy.data_ptr<float>(), bf(dx), N, (int)(H * W), C, cur_stream(dy), splits);
   return dx;
+}
+
+// ---------------------------------------------------------------------- fc
+static void check_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), name, " must be contiguous fp32");
+}
+
+// logits[N][V] = pooled[N][C] . W[V][C]^T + b
+Tensor fc_forward(const Tensor& pooled, const Tensor& w, const Tensor& b) {
+  check_f32(pooled, "pooled"); check_f32(w, "weight"); check_f32(b, "bias");
+  TORCH_CHECK(pooled.dim() == 2 && w.dim() == 2 && w.size(1) == pooled.size(1) && b.numel() == w.size(0),
+              "fc_forward: pooled [N, C], weight [V, C], bias [V]");
+  c10::hip::HIPGuard g(pooled.get_device());
+  const int N = pooled.size(0), C = pooled.size(1), V = w.size(0);
+  auto out = at::empty({N, V}, pooled.options());
+  pdt::FcArgs a{};
+  a.a = pooled.data_ptr<float>(); a.b = w.data_ptr<float>(); a.c = out.data_ptr<float>();
+  a.bias = b.data_ptr<float>();
+  a.M = N; a.N = V; a.K = C; a.sam = C; a.sak = 1; a.sbn = C; a.sbk = 1; a.ldc = V;
+  a.splits = pdt::fc_splits(N, V, C);
+  a.kper = (C + a.splits - 1) / a.splits;
+  a.kper = (a.kper + 31) / 32 * 32;
+  a.splits = (C + a.kper - 1) / a.kper;
+  Tensor ws;
+  if (a.splits > 1) {
+    ws = at::empty({a.splits, N, V}, pooled.options());
+    a.ws = ws.data_ptr<float>();
+  }
+  hipStream_t st = cur_stream(pooled);
+  pdt::launch_fc_gemm(a, st);
+  if (a.splits > 1) pdt::launch_fc_splitk_reduce(a.ws, a.splits, N, V, a.bias, a.c, V, st);
+  return out;
+}
+
+// Backward of the fc: returns (dpooled partials [splits, N, C] for avgpool_bwd, dW, db).  dW / db
+// accumulate into `dw_out` / `db_out` when given (flat gradient views), else come back fresh.
+std::tuple<Tensor, Tensor, Tensor> fc_backward(const Tensor& dlogits, const Tensor& pooled, const Tensor& w,
+                                               const std::optional<Tensor>& dw_out,
+                                               const std::optional<Tensor>& db_out) {
+  check_f32(dlogits, "dlogits"); check_f32(pooled, "pooled"); check_f32(w, "weight");
+  const int N = dlogits.size(0), V = dlogits.size(1), C = pooled.size(1);
+  TORCH_CHECK(pooled.size(0) == N && w.size(0) == V && w.size(1) == C, "fc_backward: shape mismatch");
+  c10::hip::HIPGuard g(dlogits.get_device());
+  hipStream_t st = cur_stream(dlogits);
+  Tensor dw, db;
+  const bool acc_w = dw_out.has_value() && dw_out->defined();
+  const bool acc_b = db_out.has_value() && db_out->defined();
+  if (acc_w) {
+    TORCH_CHECK(dw_out->scalar_type() == at::kFloat && dw_out->numel() == (int64_t)V * C &&
+                dw_out->stride(0) == C && dw_out->stride(1) == 1, "dw_out must be fp32 [V, C] row-major");
+    dw = *dw_out;
+  } else {
+    dw = at::empty({V, C}, w.options());
+  }
+  if (acc_b) {
+    TORCH_CHECK(db_out->scalar_type() == at::kFloat && db_out->numel() == V && db_out->is_contiguous(),
+                "db_out must be contiguous fp32 [V]");
+    db = *db_out;
+  } else {
+    db = at::empty({V}, w.options());
+  }
+  // dW[V][C] (+)= dlogits^T . pooled: A(m = v, k = n) = dlogits[n][v], B(k = n, n = c) = pooled[n][c]
+  pdt::FcArgs a{};
+  a.a = dlogits.data_ptr<float>(); a.b = pooled.data_ptr<float>(); a.c = dw.data_ptr<float>();
+  a.M = V; a.N = C; a.K = N; a.sam = 1; a.sak = V; a.sbn = 1; a.sbk = C; a.ldc = C;
+  a.splits = 1; a.kper = N; a.accumulate = acc_w ? 1 : 0;
+  if (acc_w == acc_b) {  // db from the same pass (shares the accumulate flag)
+    a.db = db.data_ptr<float>();
+    pdt::launch_fc_gemm(a, st);
+  } else {
+    pdt::launch_fc_gemm(a, st);
+    pdt::launch_fc_colsum(dlogits.data_ptr<float>(), N, V, nullptr, db.data_ptr<float>(), acc_b, st);
+  }
+  // dpooled[N][C] = dlogits . W: A(m = n, k = v) = dlogits[n][v], B(k = v, n = c) = W[v][c]
+  pdt::FcArgs d{};
+  d.a = dlogits.data_ptr<float>(); d.b = w.data_ptr<float>();
+  d.M = N; d.N = C; d.K = V; d.sam = V; d.sak = 1; d.sbn = 1; d.sbk = C; d.ldc = C;
+  d.splits = pdt::fc_splits(N, C, V);
+  d.kper = ((V + d.splits - 1) / d.splits + 31) / 32 * 32;
+  d.splits = (V + d.kper - 1) / d.kper;
+  auto dp = at::empty({d.splits, N, C}, dlogits.options());
+  if (d.splits > 1) d.ws = dp.data_ptr<float>();
+  else d.c = dp.data_ptr<float>();
+  pdt::launch_fc_gemm(d, st);
+  return {dp, dw, db};
 }
 
 // -------------------------------------------------------------------- head
@@ -777,6 +867,24 @@ std::tuple<Tensor, Tensor> softmax_xent(const Tensor& logits_in, const Tensor& l
   pdt::launch_softmax_xent(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
                            dl.data_ptr<float>(), ws.data_ptr<float>(), N, V, cur_stream(logits));
   return {loss, dl};
+}
+
+// x * alpha for a device scalar alpha (the upstream gradient of the loss), fp32
+Tensor scale_by(const Tensor& x, const Tensor& alpha) {
+  check_f32(x, "x");
+  check_cuda(alpha, "alpha");
+  TORCH_CHECK(alpha.scalar_type() == at::kFloat && alpha.numel() == 1, "alpha must be a device fp32 scalar");
+  c10::hip::HIPGuard g(x.get_device());
+  auto y = at::empty_like(x);
+  pdt::launch_scale(x.data_ptr<float>(), alpha.data_ptr<float>(), y.data_ptr<float>(), x.numel(), cur_stream(x));
+  return y;
+}
+
+void add_one_i64(Tensor x) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kLong && x.is_contiguous(), "add_one_i64: contiguous int64");
+  c10::hip::HIPGuard g(x.get_device());
+  pdt::launch_add_one_i64(x.data_ptr<int64_t>(), x.numel(), cur_stream(x));
 }
 
 Tensor top1_correct(const Tensor& logits_in, const Tensor& labels) {
@@ -994,6 +1102,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("pool_bn_bwd_apply", checked("pool_bn_bwd_apply", &pool_bn_bwd_apply));
   m.def("avgpool_fwd", checked("avgpool_fwd", &avgpool_fwd));
   m.def("avgpool_bwd", checked("avgpool_bwd", &avgpool_bwd));
+  m.def("fc_forward", checked("fc_forward", &fc_forward), py::arg("pooled"), py::arg("weight"), py::arg("bias"));
+  m.def("fc_backward", checked("fc_backward", &fc_backward), py::arg("dlogits"), py::arg("pooled"),
+        py::arg("weight"), py::arg("dw_out") = py::none(), py::arg("db_out") = py::none());
+  m.def("scale_by", checked("scale_by", &scale_by), py::arg("x"), py::arg("alpha"));
+  m.def("add_one_i64", checked("add_one_i64", &add_one_i64), py::arg("x"));
   m.def("softmax_xent", checked("softmax_xent", &softmax_xent));
   m.def("top1_correct", checked("top1_correct", &top1_correct));
   m.def("sgd_step", checked("sgd_step", &sgd_step), py::arg("p"), py::arg("g"), py::arg("buf"),

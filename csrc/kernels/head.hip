@@ -4,6 +4,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace pdt {
 
 // one 256-thread block per row
@@ -56,6 +58,43 @@ void launch_softmax_xent(const float* logits, const int64_t* labels, float* loss
   hipLaunchKernelGGL(softmax_xent_kernel, dim3(N), dim3(256), 0, st, logits, labels, dlogits, ws, V,
                      1.f / (float)N);
   hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, st, ws, N, loss);
+}
+
+// y = x * alpha[0] (alpha on the device: no host sync for the loss gradient)
+__global__ void __launch_bounds__(256) scale_kernel(const float4* __restrict__ x, const float* __restrict__ alpha,
+                                                    float4* __restrict__ y, int64_t n4) {
+  const float a = alpha[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 v = x[i];
+    v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+    y[i] = v;
+  }
+}
+
+__global__ void scale_tail_kernel(const float* __restrict__ x, const float* __restrict__ alpha,
+                                  float* __restrict__ y, int64_t start, int64_t n) {
+  const int64_t i = start + threadIdx.x;
+  if (i < n) y[i] = x[i] * alpha[0];
+}
+
+void launch_scale(const float* x, const float* alpha, float* y, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  if (n4 > 0) {
+    const int64_t b = std::min<int64_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)b), dim3(256), 0, st, reinterpret_cast<const float4*>(x),
+                       alpha, reinterpret_cast<float4*>(y), n4);
+  }
+  if (n4 * 4 < n)
+    hipLaunchKernelGGL(scale_tail_kernel, dim3(1), dim3(64), 0, st, x, alpha, y, n4 * 4, n);
+}
+
+__global__ void __launch_bounds__(256) add_one_i64_kernel(int64_t* __restrict__ x, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] += 1;
+}
+
+void launch_add_one_i64(int64_t* x, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(add_one_i64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n);
 }
 
 __global__ void __launch_bounds__(256) top1_kernel(const float* __restrict__ logits,

@@ -143,7 +143,28 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int
 void launch_maxpool_bwd(const uint16_t* dy, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
                         int C, int Ho, int Wo, hipStream_t st);
 void launch_avgpool_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st);
-void launch_avgpool_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+// dy = sum of `splits` consecutive [N][C] partials (a split-K fc dgrad), summed in order
+void launch_avgpool_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st, int splits = 1);
+
+// ------------------------------------------------------------------ fc.hip
+// C(m, n) = alpha * sum_k A(m, k) B(k, n) (+ bias[n]) on the bf16 MFMA (fp32 accumulate), with
+// A(m, k) = a[m*sam + k*sak], B(k, n) = b[n*sbn + k*sbk]; alpha: device scalar or null (1).
+// splits > 1: slice z of K (kper each) writes ws[z][M][N], summed by fc_splitk_reduce (+ bias) or
+// by the consumer; splits == 1 writes c (row stride ldc), accumulating when `accumulate`.
+// db (optional, row-contiguous A and splits == 1 only): db[m] (+)= alpha * sum_k A(m, k), taken in
+// fp32 from the same A loads (the fc bias gradient rides on the dW product).
+struct FcArgs {
+  const float* a; const float* b; float* c; float* ws; const float* bias; const float* alpha; float* db;
+  int M, N, K;
+  int64_t sam, sak, sbn, sbk;
+  int ldc, splits, kper, accumulate;
+};
+int fc_splits(int M, int N, int K);
+void launch_fc_gemm(const FcArgs& a, hipStream_t st);
+void launch_fc_splitk_reduce(const float* ws, int splits, int M, int N, const float* bias, float* c,
+                             int ldc, hipStream_t st);
+void launch_fc_colsum(const float* g, int rows, int cols, const float* alpha, float* db, bool accumulate,
+                      hipStream_t st);
 
 // ---------------------------------------------------------------- head.hip
 // loss[0] = mean CE, dlogits = (softmax - onehot)/N ; ws >= N floats
@@ -151,6 +172,10 @@ void launch_softmax_xent(const float* logits, const int64_t* labels, float* loss
                          float* ws, int N, int V, hipStream_t st);
 void launch_top1(const float* logits, const int64_t* labels, int64_t* count, int N, int V,
                  hipStream_t st);
+// x[i] += 1 (the BatchNorm num_batches_tracked counters, one flat int64 buffer)
+void launch_add_one_i64(int64_t* x, int64_t n, hipStream_t st);
+// y = x * alpha[0], alpha a device scalar (x, y 16-byte aligned fp32)
+void launch_scale(const float* x, const float* alpha, float* y, int64_t n, hipStream_t st);
 
 // ----------------------------------------------------------------- sgd.hip
 // torch.optim.SGD on flat fp32 buffers; grad is scaled by grad_scale first.

@@ -127,15 +127,22 @@ __global__ void __launch_bounds__(256) avgpool_fwd_kernel(const uint16_t* __rest
 
 __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restrict__ dy,
                                                           uint4* __restrict__ dx, int HW, int C8,
-                                                          int64_t nvec, float inv) {
+                                                          int64_t nvec, float inv, int splits,
+                                                          int64_t split_stride) {
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
     int c8 = (int)(v % C8);
     int64_t n = v / ((int64_t)C8 * HW);
     const float* g = dy + n * C8 * 8 + c8 * 8;
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = g[j];
+    for (int z = 1; z < splits; ++z)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += g[z * split_stride + j];
     f8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o.v[j] = g[j] * inv;
+    for (int j = 0; j < 8; ++j) o.v[j] = s[j] * inv;
     dx[v] = pack8(o);
   }
 }
@@ -144,11 +151,12 @@ void launch_avgpool_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipSt
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ceil_div(C, 256), N), dim3(256), 0, st, x, y, HW, C);
 }
 
-void launch_avgpool_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+void launch_avgpool_bwd(const float* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st, int splits) {
   int64_t nvec = (int64_t)N * HW * C / 8;
   int64_t b = (nvec + 255) / 256;
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3((unsigned)(b < 8192 ? b : 8192)), dim3(256), 0, st,
-                     dy, reinterpret_cast<uint4*>(dx), HW, C / 8, nvec, 1.f / (float)HW);
+                     dy, reinterpret_cast<uint4*>(dx), HW, C / 8, nvec, 1.f / (float)HW, splits,
+                     (int64_t)N * C);
 }
 
 }  // namespace pdt

@@ -310,6 +310,7 @@ class _StemConvBNPool(torch.autograd.Function):
         _nan_trace("stem+pool", x=x, xsp=xsp, y=y, part=part, stats=stats, out=out)
         ctx.save_for_backward(xsp, y, stats, gamma, idx)
         ctx.weight = weight
+        ctx.bn_params = (gamma, beta)
         ctx.training = training
         return out
 
@@ -318,21 +319,31 @@ class _StemConvBNPool(torch.autograd.Function):
         C = native()
         xsp, y, stats, gamma, idx = ctx.saved_tensors
         weight = ctx.weight
+        gp, bp = ctx.bn_params
+        ctx.bn_params = None
         dout = dout.contiguous()
-        sums = C.pool_bn_bwd_reduce(dout, idx, y, stats)
-        dgamma, dbeta = sums[1] * stats[1], sums[0]
+        sg, sb = _grad_sink(gp), _grad_sink(bp)
+        sunk = []
+        if sg is not None and sb is not None:  # BN parameter gradients straight into the flat buffer
+            sums = C.pool_bn_bwd_reduce(dout, idx, y, stats, sg, sb)
+            dgamma = dbeta = None
+            sunk += [gp, bp]
+        else:
+            sums = C.pool_bn_bwd_reduce(dout, idx, y, stats)
+            dgamma, dbeta = (sums[1] * stats[1]).to(gamma.dtype), sums[0].to(gamma.dtype)
         dy = C.pool_bn_bwd_apply(dout, idx, y, stats, gamma, sums, ctx.training)
         dw = None
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(weight)
             if sink is not None:
                 C.stem_wgrad(dy, xsp, list(weight.shape), deterministic(), sink)
-                weight._pdt_flat.mark_ready([weight])
+                sunk.append(weight)
             else:
                 dw = C.stem_wgrad(dy, xsp, list(weight.shape), deterministic()).to(weight.dtype)
+        if sunk:
+            sunk[0]._pdt_flat.mark_ready(sunk)
         ctx.weight = None
-        return (None, dw, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, None, None, None,
-                None, None, None)
+        return (None, dw, dgamma, dbeta, None, None, None, None, None, None, None)
 
 
 _STEM_POOL = os.environ.get("PDT_STEM_POOL", "1") != "0"  # debugging switch (default on)
@@ -412,29 +423,51 @@ def maxpool3x3s2(x: torch.Tensor) -> torch.Tensor:
 # global avg pool + fc
 # ----------------------------------------------------------------------------
 class _AvgPoolLinear(torch.autograd.Function):
+    """Global average pool + the classifier Linear (torchvision fc, resnet/main.py:76).
+
+    Device path: avg-pool kernel, then the hand-written fc GEMMs of ``csrc/kernels/fc.hip`` (bf16
+    MFMA, fp32 accumulation) -- forward with the bias folded into its split-K reduction; backward
+    dW (accumulated straight into the flat gradient buffer under DDP), db, and the input gradient,
+    whose split-K partials the avg-pool backward sums while broadcasting over H x W.  No library
+    GEMM and no ATen kernel runs for the head."""
+
     @staticmethod
     def forward(ctx, x, weight, bias):
         if x.is_cuda:
-            pooled = native().avgpool_fwd(x)           # fp32 [N, C]
+            C = native()
+            pooled = C.avgpool_fwd(x)           # fp32 [N, C]
+            logits = C.fc_forward(pooled, weight.float().contiguous(), bias.float().contiguous())
         else:
             pooled = ref.global_avgpool(x)
-        logits = torch.addmm(bias.float(), pooled, weight.float().t())
+            logits = torch.addmm(bias.float(), pooled, weight.float().t())
         ctx.save_for_backward(pooled, weight)
+        ctx.params = (weight, bias)
         ctx.hw = (x.shape[1], x.shape[2], x.dtype)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         pooled, weight = ctx.saved_tensors
+        wp, bp = ctx.params
+        ctx.params = None
         h, w, dt = ctx.hw
         dlogits = dlogits.float().contiguous()
+        if dlogits.is_cuda:
+            C = native()
+            sw, sb = _grad_sink(wp), _grad_sink(bp)
+            if sw is not None and sb is not None and sw.is_contiguous():
+                dp, _, _ = C.fc_backward(dlogits, pooled, weight.float().contiguous(), sw, sb)
+                wp._pdt_flat.mark_ready([wp, bp])
+                dw = db = None
+            else:
+                dp, dw, db = C.fc_backward(dlogits, pooled, weight.float().contiguous())
+                dw, db = dw.to(weight.dtype), db.to(weight.dtype)
+            dx = C.avgpool_bwd(dp, h, w)
+            return dx, dw, db
         dw = dlogits.t().mm(pooled)
         db = dlogits.sum(0)
         dpooled = dlogits.mm(weight.float())
-        if dlogits.is_cuda:
-            dx = native().avgpool_bwd(dpooled, h, w)
-        else:
-            dx = (dpooled / (h * w))[:, None, None, :].expand(-1, h, w, -1).to(dt).contiguous()
+        dx = (dpooled / (h * w))[:, None, None, :].expand(-1, h, w, -1).to(dt).contiguous()
         return dx, dw.to(weight.dtype), db.to(weight.dtype)
 
 
@@ -458,6 +491,8 @@ class _SoftmaxXent(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         (dlogits,) = ctx.saved_tensors
+        if dlogits.is_cuda:  # scaled on the device by the (device) loss gradient: no host sync
+            return native().scale_by(dlogits, dloss.float().reshape(1)), None
         return dlogits * dloss, None
 
 
@@ -509,7 +544,26 @@ def buffers_ready() -> None:
     if _PENDING_BUMP is not None:
         counters, _PENDING_BUMP = _PENDING_BUMP, None
         with torch.no_grad():
-            torch._foreach_add_(counters, 1)
+            flat = _counter_flat(counters)
+            if flat is not None:   # every counter is a view of one int64 buffer (DDP): one launch
+                native().add_one_i64(flat)
+            else:
+                torch._foreach_add_(counters, 1)
+
+
+def _counter_flat(counters):
+    """The int64 buffer that exactly holds ``counters`` as consecutive one-element views (what
+    ``parallel.flat.flatten_buffers`` builds when every int64 buffer is a BN counter), else None."""
+    if not counters or not counters[0].is_cuda:
+        return None
+    base = counters[0]._base
+    if base is None or base.dtype != torch.int64 or base.numel() != len(counters):
+        return None
+    p0 = base.data_ptr()
+    for i, c in enumerate(counters):
+        if c._base is not base or c.data_ptr() != p0 + 8 * i:
+            return None
+    return base
 
 
 class bump_bn_counters:

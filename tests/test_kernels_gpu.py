@@ -710,3 +710,47 @@ def test_compact_stride2_addend(gpu, native_ext, cfg):
     a = C.conv_dgrad_bn(dy, wt, [n, h, w, c], st, pd, comp, y, None, stats, 2)
     b = C.conv_dgrad_bn(dy, wt, [n, h, w, c], st, pd, full, y, None, stats, 2)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("n,c,v", [(256, 2048, 1000), (32, 512, 10), (7, 72, 33)])
+def test_fc_gemms_match_fp32_linear(gpu, native_ext, n, c, v):
+    """Hand-written head GEMMs (bf16 MFMA, fp32 accumulate, split-K) vs fp32 F.linear and its
+    gradients; dW/db accumulate into given buffers; the dgrad partials feed avgpool_bwd."""
+    C = native_ext
+    g = torch.Generator().manual_seed(31)
+    pooled = torch.randn(n, c, generator=g).to(gpu)
+    w = (torch.randn(v, c, generator=g) / c ** 0.5).to(gpu)
+    b = torch.randn(v, generator=g).to(gpu)
+    logits = C.fc_forward(pooled, w, b)
+    assert _rel_err(logits, F.linear(pooled, w, b)) < 1e-2
+    dl = (torch.randn(n, v, generator=g) * 1e-2).to(gpu)
+    dp, dw, db = C.fc_backward(dl, pooled, w)
+    assert _rel_err(dw, dl.t() @ pooled) < 1e-2
+    assert torch.allclose(db, dl.sum(0), rtol=1e-5, atol=1e-6)
+    assert _rel_err(dp.sum(0), dl @ w) < 1e-2
+    dw0, db0 = torch.randn(v, c, device=gpu), torch.randn(v, device=gpu)
+    dw1, db1 = dw0.clone(), db0.clone()
+    C.fc_backward(dl, pooled, w, dw1, db1)
+    assert torch.allclose(dw1, dw0 + dw, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(db1, db0 + db, rtol=1e-5, atol=1e-6)
+    dx = C.avgpool_bwd(dp, 3, 5)
+    ref_dx = ((dl @ w) / 15)[:, None, None, :].expand(n, 3, 5, c)
+    assert _rel_err(dx, ref_dx) < 1.5e-2
+
+
+def test_avgpool_linear_and_ce_autograd(gpu, native_ext):
+    from pytorch_distributed_tutorials_amd import ops
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(16, 7, 7, 256, generator=g).to(torch.bfloat16).to(gpu).requires_grad_(True)
+    w = (torch.randn(100, 256, generator=g) * 0.05).to(gpu).requires_grad_(True)
+    b = torch.randn(100, generator=g).to(gpu).requires_grad_(True)
+    y = torch.randint(0, 100, (16,), generator=g).to(gpu)
+    loss = ops.cross_entropy(ops.avgpool_linear(x, w, b), y) * 3.0   # non-unit upstream gradient
+    loss.backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr, br = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    lr = F.cross_entropy(F.linear(xr.mean((1, 2)), wr, br), y) * 3.0
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 1e-2 * lr.item()
+    assert _rel_err(w.grad, wr.grad) < 1e-2 and _rel_err(b.grad, br.grad) < 1e-2
+    assert _rel_err(x.grad, xr.grad) < 2e-2
