@@ -4,6 +4,7 @@ from .datasets import (  # noqa: F401
     TensorImageDataset,
     build_dataset,
     cifar10,
+    learnable_dataset,
     synthetic_dataset,
 )
 from .loader import DeviceLoader, draw_crop_flip, random_crop_flip  # noqa: F401

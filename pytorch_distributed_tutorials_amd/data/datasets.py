@@ -51,6 +51,21 @@ def synthetic_dataset(num_samples: int, image_size: int, num_classes: int,
     return TensorImageDataset(imgs.to(device), labels.to(device), normalized=True)
 
 
+def learnable_dataset(num_samples: int, image_size: int, num_classes: int, device="cpu", seed: int = 0,
+                      noise: float = 1.0, template_seed: int = 12345) -> TensorImageDataset:
+    """A synthetic set a network can actually learn (convergence checks without CIFAR on disk):
+    class c's images are a fixed random template t_c (shared by train and test splits through
+    ``template_seed``) plus i.i.d. Gaussian noise of std ``noise``; normalized float images."""
+    gt = torch.Generator(device="cpu")
+    gt.manual_seed(template_seed)
+    templates = torch.randn((num_classes, 3, image_size, image_size), generator=gt)
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    labels = torch.randint(0, num_classes, (num_samples,), generator=g)
+    imgs = templates[labels] + noise * torch.randn((num_samples, 3, image_size, image_size), generator=g)
+    return TensorImageDataset(imgs.to(device), labels.to(device), normalized=True)
+
+
 class _NumpyOnlyUnpickler(pickle.Unpickler):
     """CIFAR-10 python batches are pickled dicts of numpy arrays; refuse anything else."""
     _ALLOWED = {
@@ -102,7 +117,8 @@ def cifar10(root: str = "data", train: bool = True) -> TensorImageDataset:
 def build_dataset(kind: str, train: bool, root: str = "data", num_samples: Optional[int] = None,
                   image_size: Optional[int] = None, num_classes: int = 10,
                   seed: int = 0) -> TensorImageDataset:
-    """kind: 'cifar10' (disk), 'synthetic-cifar' (32px) or 'synthetic-imagenet' (224px)."""
+    """kind: 'cifar10' (disk), 'synthetic-cifar' (32px), 'synthetic-imagenet' (224px), or
+    'learnable-cifar' (32px class templates + noise: a set the model can fit)."""
     if kind == "cifar10":
         return cifar10(root, train)
     if kind == "synthetic-cifar":
@@ -111,4 +127,7 @@ def build_dataset(kind: str, train: bool, root: str = "data", num_samples: Optio
     if kind == "synthetic-imagenet":
         n = num_samples or (2048 if train else 512)
         return synthetic_dataset(n, image_size or 224, num_classes, seed=seed + (0 if train else 1))
+    if kind == "learnable-cifar":
+        n = num_samples or (10000 if train else 2000)
+        return learnable_dataset(n, image_size or 32, num_classes, seed=seed + (0 if train else 1))
     raise ValueError(f"unknown dataset kind {kind!r}")

@@ -69,7 +69,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--impl", default="auto", choices=["auto", "native", "torch"],
                    help="native = MI355X HIP kernels (GPU); torch = stock ATen ops")
     p.add_argument("--data", default="cifar10",
-                   choices=["cifar10", "synthetic-cifar", "synthetic-imagenet"])
+                   choices=["cifar10", "synthetic-cifar", "synthetic-imagenet", "learnable-cifar"])
     p.add_argument("--data-root", default="data")
     p.add_argument("--synthetic-samples", type=int, default=None)
     p.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])

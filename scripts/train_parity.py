@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Training-level parity: the native bf16 path vs the stock fp32 path, same init, same data.
+
+Trains ResNet-18 (the reference model, resnet/main.py:76) on a learnable synthetic CIFAR-shaped
+set (class templates + noise, ``data.learnable_dataset``) with the reference optimizer
+(SGD lr 0.01, momentum 0.9, wd 1e-5, resnet/main.py:103) for ``--steps`` steps:
+
+* native: our NHWC bf16 kernels, our DDP wrapper (world 1: flat buffers, in-place gradient
+  sinks), fused SGD;
+* stock:  the same weights as a plain fp32 torch model (impl="torch") with torch.optim.SGD.
+
+Both see identical batches (one fixed permutation per epoch).  Prints one JSON line with the
+per-window mean losses of both runs and the final train accuracy (eval mode, whole set).
+
+    python scripts/train_parity.py [--steps 200] [--batch 128] [--json out.json]
+"""
+import argparse
+import copy
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_tutorials_amd import ops  # noqa: E402
+from pytorch_distributed_tutorials_amd.data import learnable_dataset  # noqa: E402
+from pytorch_distributed_tutorials_amd.models import build_model  # noqa: E402
+from pytorch_distributed_tutorials_amd.optim import SGD  # noqa: E402
+from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel  # noqa: E402
+
+
+def accuracy(model, ds, native, bs=500):
+    model.eval()
+    correct = 0
+    with torch.no_grad():
+        for i in range(0, len(ds), bs):
+            x, y = ds.images[i:i + bs], ds.labels[i:i + bs]
+            out = model(x)
+            correct += int((ops.top1_correct(out, y) if native else (out.argmax(1) == y).sum()).item())
+    model.train()
+    return correct / len(ds)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--samples", type=int, default=4096)
+    ap.add_argument("--noise", type=float, default=1.0)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--window", type=int, default=20)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    ds = learnable_dataset(a.samples, 32, 10, device=dev, seed=3, noise=a.noise)
+    torch.manual_seed(0)
+    stock = build_model("resnet18", num_classes=10).to(dev)
+    native_m = copy.deepcopy(stock).set_impl("native")
+    native = DistributedDataParallel(native_m)          # world 1: flat space + grad sinks
+    opt_n = SGD(native.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
+    opt_s = torch.optim.SGD(stock.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
+    g = torch.Generator().manual_seed(11)
+    perm = torch.randperm(len(ds), generator=g).to(dev)
+    pos = 0
+    ln, ls = [], []
+    for step in range(a.steps):
+        if pos + a.batch > len(ds):
+            perm = torch.randperm(len(ds), generator=g).to(dev)
+            pos = 0
+        idx = perm[pos:pos + a.batch]
+        pos += a.batch
+        x, y = ds.images[idx], ds.labels[idx]
+        opt_n.zero_grad()
+        loss_n = ops.cross_entropy(native(x), y)
+        loss_n.backward()
+        opt_n.step()
+        opt_s.zero_grad()
+        loss_s = F.cross_entropy(stock(x), y)
+        loss_s.backward()
+        opt_s.step()
+        ln.append(loss_n.detach())
+        ls.append(loss_s.detach())
+    ln = torch.stack(ln).float().cpu()
+    ls = torch.stack(ls).float().cpu()
+    w = a.window
+    nwin = a.steps // w
+    res = {
+        "steps": a.steps, "batch": a.batch, "samples": a.samples, "noise": a.noise, "lr": a.lr,
+        "window": w,
+        "native_window_loss": [round(float(ln[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],
+        "stock_window_loss": [round(float(ls[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],
+        "native_train_acc": accuracy(native, ds, True),
+        "stock_train_acc": accuracy(stock, ds, False),
+        "finite": bool(torch.isfinite(ln).all() and torch.isfinite(ls).all()),
+    }
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()

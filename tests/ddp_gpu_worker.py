@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--image", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--learn", type=int, default=0,
+                    help="then train this many steps on a learnable set, sharded over ranks, and "
+                         "record the cross-rank parameter checksums every 20 steps")
     a = ap.parse_args()
     env = init_distributed("gloo")
     rank, world = env.rank, env.world_size
@@ -91,7 +94,33 @@ def main():
                       dtype=torch.float64)
     all_cs = [torch.zeros_like(cs) for _ in range(world)]
     dist.all_gather(all_cs, cs)
+    learn_cs, learn_loss = [], []
+    if a.learn:
+        from pytorch_distributed_tutorials_amd.data import DistributedSampler, learnable_dataset
+        ds = learnable_dataset(2048, a.image, 10, device=dev, seed=5)
+        sampler = DistributedSampler(len(ds), num_replicas=world, rank=rank, shuffle=True, seed=0)
+        order, epoch = [], 0
+        for step in range(a.learn):
+            if len(order) < a.batch:
+                sampler.set_epoch(epoch)
+                epoch += 1
+                order += list(iter(sampler))
+            idx = torch.tensor(order[:a.batch], device=dev)
+            order = order[a.batch:]
+            opt.zero_grad()
+            loss = ops.cross_entropy(ddp(ds.images[idx]), ds.labels[idx])
+            loss.backward()
+            opt.step()
+            if step % 20 == 19 or step == a.learn - 1:
+                torch.cuda.synchronize()
+                c = torch.tensor([float(sum(p.detach().double().sum().item() for p in ddp.parameters()))],
+                                 dtype=torch.float64)
+                cs_all = [torch.zeros_like(c) for _ in range(world)]
+                dist.all_gather(cs_all, c)
+                learn_cs.append([float(v.item()) for v in cs_all])
+                learn_loss.append(float(loss.item()))
     res = {"rank": rank, "world": world, "grad_rel_err": rel, "worst_params": per[:5],
+           "learn_checksums": learn_cs, "learn_loss": learn_loss,
            "checksums": [float(c.item()) for c in all_cs],
            "launch_order": list(ddp.reducer.last_launch_order()),
            "bucket_info": ddp.bucket_info(),

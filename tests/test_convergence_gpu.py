@@ -1,0 +1,53 @@
+"""Training-level parity: the native bf16 path learns like the stock fp32
+path from the same init on the same data, and data-parallel ranks stay bit-identical while
+training.  Uses ``scripts/train_parity.py`` (ResNet-18, learnable synthetic CIFAR-shaped set --
+real CIFAR-10 is not on the box, so CIFAR accuracy itself is parity-unpinned)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+from conftest import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def test_native_bf16_training_tracks_stock_fp32(gpu, tmp_path):
+    out = tmp_path / "parity.json"
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_parity.py"), "--steps", "200",
+                        "--json", str(out)], cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["finite"]
+    n, s = res["native_window_loss"], res["stock_window_loss"]
+    # both learn: the loss falls by >10x from the first window, both fit the training set
+    assert n[-1] < 0.1 * n[0] and s[-1] < 0.1 * s[0], (n, s)
+    assert res["native_train_acc"] > 0.9 and res["stock_train_acc"] > 0.9, res
+    # tolerance band: every 20-step window mean within 0.15 + 25 % of the stock curve
+    for a, b in zip(n, s):
+        assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)
+
+
+def test_two_ranks_stay_bit_identical_while_training(gpu, tmp_path):
+    out = str(tmp_path / "res")
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "ddp_gpu_worker.py"), "--out", out, "--arch", "resnet18",
+           "--image", "32", "--batch", "64", "--learn", "60"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=170, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(f"{out}.rank{i}.json")) for i in range(2)]
+    for x in res:
+        assert x["finite"]
+    hist = res[0]["learn_checksums"]
+    assert len(hist) >= 3
+    for h in hist:  # every checkpoint: both ranks' parameter checksums equal
+        assert h[0] == h[1], hist
+    assert res[0]["learn_loss"][-1] < res[0]["learn_loss"][0], res[0]["learn_loss"]
