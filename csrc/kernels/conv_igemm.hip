@@ -212,8 +212,26 @@ __device__ __forceinline__ void wait_steps(int younger) {
 // MFMA operands are swapped (A = weights, B = pixels) so each lane's 4 accumulator registers are
 // 4 consecutive output channels of one pixel: the epilogue packs them into one 8-byte LDS write
 // and the BN statistics reduce over the 16 pixel-lanes with DPP-friendly xor shuffles.
+// Minimum waves per SIMD the register allocator must leave room for (launch bounds).  With the
+// default (1) hipcc parks the accumulators in AGPRs and allocates 204-232 registers per lane for
+// the 4-wave tiles (2 waves per SIMD); a floor of 2 gives the same code in 115 (stats / plain
+// epilogue) and 168 (BN-backward epilogue) VGPRs, no spills, so the one-K-step 1x1 convs (whose
+// LDS fits 4 blocks) run 3-4 blocks per CU: layer1 64->256 fwd 147 -> 130 us, 256->64 BN dgrad
+// 234 -> 200 us, ResNet-50 step 20.50 -> 20.35 ms (r2v).  The 8-wave tile is LDS-bound at one
+// block per CU either way.  PDT_NT_OCC4 / PDT_NT_OCC8 are build-time tuning knobs.
+#ifndef PDT_NT_OCC4
+#define PDT_NT_OCC4 2
+#endif
+#ifndef PDT_NT_OCC8
+#define PDT_NT_OCC8 1
+#endif
+template <int WAVES, bool HALO>
+constexpr int nt_min_waves() {
+  return WAVES == 4 ? (HALO ? 2 : PDT_NT_OCC4) : PDT_NT_OCC8;
+}
+
 template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool HALO = false>
-__global__ void __launch_bounds__(WM * WN * 64, (HALO && WM * WN == 4) ? 2 : 1) igemm_nt_kernel(const NtArgs P) {
+__global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>())) igemm_nt_kernel(const NtArgs P) {
   static_assert(!HALO || (C64 && OP == OP_BF16), "halo staging: bf16, 64-channel blocks");
   using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
   constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
