@@ -158,18 +158,33 @@ constexpr int EPI_BNB = 2;    // + fused BN backward relu-mask and partial sums 
 __device__ __forceinline__ int swz128(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
+// [rows][32] bf16 (K32 stages): 64-B rows, chunk XOR (row>>2)&3 -- the 16 rows of a fragment
+// read cover (row&3, chunk^((row>>2)&3)) = all 16 slots of the bank row: conflict-free.
+__device__ __forceinline__ int swz64(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+template <bool K32>
+__device__ __forceinline__ int swz_row(int row, int chunk) {
+  if constexpr (K32) return swz64(row, chunk);
+  else return swz128(row, chunk);
+}
 
-template <int WM, int WN, int TM, int TN, int STAGES = 2>
+// K32: a K-step is 32 bf16 (64-B operand rows) instead of 64 (128-B rows).  Same LDS per stage
+// pair, so the ring can be twice as deep for the same footprint: a 4-stage K32 ring keeps three
+// steps of loads in flight where the 2-stage K64 ring keeps one (one barrier per 32 of K).
+template <int WM, int WN, int TM, int TN, int STAGES = 2, bool K32 = false>
 struct NtCfg {
   static constexpr int NT = WM * WN * 64;
   static constexpr int WAVES = WM * WN;
   static constexpr int BM = WM * TM * 16;
   static constexpr int BN = WN * TN * 16;
-  // one LDS-DMA wave instruction moves 64 lanes x 16 B = 8 rows of a [rows][64] bf16 tile
-  static constexpr int A_PW = BM / 8 / WAVES;  // instructions per wave per K-step
-  static constexpr int B_PW = BN / 8 / WAVES;
-  static_assert(A_PW * 8 * WAVES == BM && B_PW * 8 * WAVES == BN, "tile rows must split over waves");
-  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int ROWB = K32 ? 64 : 128;  // bytes per operand row per K-step
+  static constexpr int RPI = 1024 / ROWB;      // rows per LDS-DMA wave instruction (64 x 16 B)
+  static constexpr int LPR = ROWB / 16;        // lanes per row in one instruction
+  static constexpr int A_PW = BM / RPI / WAVES;  // instructions per wave per K-step
+  static constexpr int B_PW = BN / RPI / WAVES;
+  static_assert(A_PW * RPI * WAVES == BM && B_PW * RPI * WAVES == BN, "tile rows must split over waves");
+  static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
   static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row (pixel)
   static constexpr int EPI_BYTES = WAVES * (TM * 16) * EPI_PITCH;
@@ -197,10 +212,12 @@ __device__ __forceinline__ void wait_vm() {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 // Multi-stage pipelines: every K-step issues LPS DMA ops per wave; wait until the oldest pending
-// step has landed while `younger` later steps (wave-uniform, < 3) may stay in flight.
+// step has landed while `younger` later steps (wave-uniform, < 5) may stay in flight.
 template <int LPS>
 __device__ __forceinline__ void wait_steps(int younger) {
-  if (younger >= 2) wait_vm<2 * LPS>();
+  if (younger >= 4) wait_vm<4 * LPS>();
+  else if (younger == 3) wait_vm<3 * LPS>();
+  else if (younger == 2) wait_vm<2 * LPS>();
   else if (younger == 1) wait_vm<LPS>();
   else wait_vm<0>();
 }
@@ -230,13 +247,16 @@ constexpr int nt_min_waves() {
   return WAVES == 4 ? (HALO ? 2 : PDT_NT_OCC4) : PDT_NT_OCC8;
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool HALO = false>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool HALO = false,
+          bool K32 = false>
 __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>())) igemm_nt_kernel(const NtArgs P) {
   static_assert(!HALO || (C64 && OP == OP_BF16), "halo staging: bf16, 64-channel blocks");
-  using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
+  static_assert(!K32 || (OP == OP_BF16 && !HALO), "K32 stages: bf16 per-tap staging only");
+  using CFG = NtCfg<WM, WN, TM, TN, STAGES, K32>;
   constexpr int BM = CFG::BM, BN = CFG::BN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
+  constexpr int RPI = CFG::RPI, LPR = CFG::LPR;
   constexpr int EB = OP == OP_BF16 ? 2 : 1;  // bytes per element
-  constexpr int KE = 128 / EB;               // elements per K-step (one 128-byte row)
+  constexpr int KE = CFG::ROWB / EB;         // elements per K-step (one operand row)
   constexpr int CE = 16 / EB;                // elements per 16-byte chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -250,7 +270,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   // wave id through readfirstlane: uniform for the compiler, so every LDS-DMA destination
   // (tile base + wave slot) is scalar math + one m0 write, no VGPR add + readfirstlane per load
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int lr = lane >> 3, lj = lane & 7;
+  const int lr = lane / LPR, lj = lane % LPR;  // row within a DMA instruction, LDS chunk slot
+  // source chunk that lands in LDS slot lj of row `row` (the read side applies the same XOR)
+  auto src_chunk = [&](int row) { return K32 ? (lj ^ ((row >> 2) & 3)) : (lj ^ ((row >> 1) & 7)); };
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
@@ -261,8 +283,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   int a_pix[A_PW], a_h0[A_PW], a_w0[A_PW], a_c[A_PW], a_base[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
-    const int row = (wid * A_PW + i) * 8 + lr;
-    a_c[i] = lj ^ ((row >> 1) & 7);
+    const int row = (wid * A_PW + i) * RPI + lr;
+    a_c[i] = src_chunk(row);
     const int m = m0 + row;
     if (m < P.M) {
       uint32_t n = fdiv((uint32_t)m, P.div_ij);
@@ -280,8 +302,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   int b_row[B_PW], b_c[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
-    const int row = (wid * B_PW + i) * 8 + lr;
-    b_c[i] = lj ^ ((row >> 1) & 7);
+    const int row = (wid * B_PW + i) * RPI + lr;
+    b_c[i] = src_chunk(row);
     const int n = n0 + row;
     b_row[i] = n < P.Nout ? n * P.Kg : -1;
   }
@@ -337,8 +359,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   int k_ti = 0, k_tj = 0, k_chb = 0;
 
   auto issue = [&](int kt, int buf) {
-    char* As = smem + buf * (BM + BN) * 128;
-    char* Bs = As + BM * 128;
+    char* As = smem + buf * CFG::STAGE_BYTES;
+    char* Bs = As + BM * CFG::ROWB;
     if constexpr (C64) {
       const int tap = k_ti * P.tns + k_tj;
       const int dr = P.dr0 + k_ti * P.dstep, ds = P.ds0 + k_tj * P.dstep;
@@ -523,18 +545,18 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, nxt);
     const char* As = smem + cur * CFG::STAGE_BYTES;
-    const char* Bs = As + BM * 128;
+    const char* Bs = As + BM * CFG::ROWB;
     if constexpr (OP == OP_BF16) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KE / 32; ++ks) {
         const int kc = ks * 4 + fq;
         v4i af[TM], bfr[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          af[i] = *reinterpret_cast<const v4i*>(As + swz128(wm * TM * 16 + i * 16 + fr, kc));
+          af[i] = *reinterpret_cast<const v4i*>(As + swz_row<K32>(wm * TM * 16 + i * 16 + fr, kc));
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz128(wn * TN * 16 + j * 16 + fr, kc));
+          bfr[j] = *reinterpret_cast<const v4i*>(Bs + swz_row<K32>(wn * TN * 16 + j * 16 + fr, kc));
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1209,12 +1231,12 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16>
+template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool K32 = false>
 static void run_nt(const NtArgs& a, hipStream_t st) {
-  using CFG = NtCfg<WM, WN, TM, TN, STAGES>;
+  using CFG = NtCfg<WM, WN, TM, TN, STAGES, K32>;
   int ntm = (a.M + CFG::BM - 1) / CFG::BM;
   int ntn = (a.Nout + CFG::BN - 1) / CFG::BN;
-  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, STAGES, C64, EPI, OP>;
+  auto kfn = igemm_nt_kernel<WM, WN, TM, TN, STAGES, C64, EPI, OP, false, K32>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -1222,7 +1244,7 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
   }
   // a K loop shorter than the pipeline never touches the last buffers: request only the LDS it
   // uses so more blocks fit per CU (the short-K 1x1 convs are bound by their epilogue stores)
-  constexpr int KE = OP == OP_BF16 ? 64 : 128;
+  constexpr int KE = OP == OP_BF16 ? (K32 ? 32 : 64) : 128;
   const int nk = C64 ? a.ntaps * (a.CA / KE) : (a.Kg + KE - 1) / KE;
   const int smem = std::max(std::max(1, std::min(nk, STAGES)) * CFG::STAGE_BYTES, CFG::EPI_BYTES);
   hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(CFG::NT), smem, st, a);
@@ -1281,18 +1303,32 @@ static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
   return true;
 }
 
-// Pipeline depth per NT tile (256x64, 64x128, 128x128); PDT_NT_STAGES="a,b,c" overrides.
-static int nt_stages(int which) {
-  static int v[3] = {-1, -1, -1};
-  if (v[0] < 0) {
-    v[0] = 2; v[1] = 2; v[2] = 2;
-    if (const char* e = getenv("PDT_NT_STAGES")) {
-      int x[3] = {2, 2, 2};
-      if (sscanf(e, "%d,%d,%d", &x[0], &x[1], &x[2]) == 3)
-        for (int k = 0; k < 3; ++k) v[k] = x[k] == 3 ? 3 : 2;
+// K-step per NT launch: K32 ring (4 stages; 5 on the 8-wave tile, 160 KB) or K64 double buffer.
+// Measured on MI355X (r2x, bench_conv.py, batch 256): the K32 ring's earlier first MFMA and
+// deeper prefetch pay on the huge-M, short-K layer1 GEMMs -- forward 64->256 1x1 136 -> 120 us,
+// 256->64 117 -> 103, and the 64-channel dgrads -- while every long-K conv loses 5-20% to the
+// doubled barriers and fragment-read restarts (256x14x14 3x3 68 -> 79 us).  Policy: K32 for
+// M >= 786432 on forward (stats epilogue) GEMMs and 64-column dgrads.  PDT_NT_K32=0/1 forces one
+// mode for every tile ("a,b,c,d" per tile: 256x64, 64x128, 256x256, 128x128).
+static int nt_k32_env(int which) {
+  static int v[4] = {-2, -2, -2, -2};
+  if (v[0] == -2) {
+    v[0] = v[1] = v[2] = v[3] = -1;  // -1: policy
+    if (const char* e = getenv("PDT_NT_K32")) {
+      int x[4];
+      if (sscanf(e, "%d,%d,%d,%d", &x[0], &x[1], &x[2], &x[3]) == 4)
+        for (int k = 0; k < 4; ++k) v[k] = x[k] ? 1 : 0;
+      else
+        v[0] = v[1] = v[2] = v[3] = atoi(e) ? 1 : 0;
     }
   }
   return v[which];
+}
+
+static bool nt_k32(int which, const NtArgs& a, int epi) {
+  const int e = nt_k32_env(which);
+  if (e >= 0) return e == 1;
+  return a.M >= 786432 && (epi == EPI_STATS || a.Nout <= 64);
 }
 
 // Tile policy.  Per K-step a BMxBN tile issues (BM+BN)/8 1-KiB LDS-DMA instructions and reads
@@ -1357,16 +1393,18 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     else run_nt<2, 2, 4, 4, 2, C64, EPI, OP>(a, st);
     return;
   }
+  const bool k32ok = C64 || !a.c8;  // the 8-channel (stem) loader packs 8 taps per K64 step
   if (a.Nout <= 64) {
-    if (nt_stages(0) == 3) run_nt<4, 1, 4, 4, 3, C64, EPI>(a, st);  // 256 x 64
+    if (k32ok && nt_k32(0, a, EPI)) run_nt<4, 1, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 256 x 64
     else run_nt<4, 1, 4, 4, 2, C64, EPI>(a, st);
   } else if (rows == 64) {
-    if (nt_stages(1) == 3) run_nt<2, 2, 2, 4, 3, C64, EPI>(a, st);  // 64 x 128
+    if (k32ok && nt_k32(1, a, EPI)) run_nt<2, 2, 2, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 64 x 128
     else run_nt<2, 2, 2, 4, 2, C64, EPI>(a, st);
   } else if (rows == 256) {
-    run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);  // 256 x 256
+    if (k32ok && nt_k32(2, a, EPI)) run_nt<4, 2, 4, 8, 5, C64, EPI, OP_BF16, true>(a, st);  // 256 x 256
+    else run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);
   } else {
-    if (nt_stages(2) == 3) run_nt<2, 2, 4, 4, 3, C64, EPI>(a, st);  // 128 x 128
+    if (k32ok && nt_k32(3, a, EPI)) run_nt<2, 2, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 128 x 128
     else run_nt<2, 2, 4, 4, 2, C64, EPI>(a, st);
   }
 }

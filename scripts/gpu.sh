@@ -13,6 +13,7 @@
 #   prof[:args]            rocprofv3 --kernel-trace --stats of bench.py <args>  -> gpurun_out/TAG_prof
 #   pmc:<counters>[:args]  one rocprofv3 --pmc pass over bench.py <args>          -> gpurun_out/TAG_pmc_N
 #   py:<script>[:args]     python -u <script> <args>
+#   env:VAR=VALUE          export VAR for the steps after it (env:VAR= unsets it)
 set -o pipefail
 TAG=${1:?tag}; shift
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -61,6 +62,10 @@ for st in "$@"; do
     py)
       s=${rest%%:*}; args=""; [ "$s" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       run "py_$(basename "$s" .py)" 900 python -u "$s" $args || exit 1 ;;
+    env)
+      var=${rest%%=*}; val=${rest#*=}
+      if [ -n "$val" ]; then export "$var=$val"; else unset "$var"; fi
+      echo "[$(date +%T)] env $var=$val" | tee -a "$O/${TAG}_status.txt" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

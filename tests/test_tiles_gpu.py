@@ -285,3 +285,50 @@ def test_bn_single_launch_reductions_match_two_launch_and_grid_caps(gpu):
     small = _run_bn({"PDT_EW_BLOCKS": "256"})      # many grid-stride iterations per thread
     assert base == two, "last-block handshake differs from the two-launch reduction"
     assert base == small, "capped grid-stride passes differ from the default grids"
+
+
+_K32_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from pytorch_distributed_tutorials_amd.ops import native
+from test_tiles_gpu import FWD_TILES, DGRAD_TILES, _operands
+C = native()
+dev = torch.device("cuda:0")
+out = {}
+for i, (shape, _) in enumerate(FWD_TILES):
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, _ = _operands(shape, dev, 1)
+    y, part = C.conv_fwd(x, C.pack_weight(wt, c), st, pd, True)
+    out[f"fwd{i}"] = (y.cpu(), part.cpu())
+for i, (shape, _) in enumerate(DGRAD_TILES):
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, dy = _operands(shape, dev, 2)
+    g = torch.Generator().manual_seed(3)
+    y = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    stats = torch.stack([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5,
+                         torch.randn(c, generator=g), torch.randn(c, generator=g) * 0.1]).to(dev).contiguous()
+    add = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    dx = C.conv_dgrad(dy, wt, list(x.shape), st, pd)
+    gk, sums = C.conv_dgrad_bn(dy, wt, list(x.shape), st, pd, add, y, None, stats, 2)
+    out[f"dgrad{i}"] = (dx.cpu(), gk.cpu(), sums.cpu())
+torch.cuda.synchronize()
+torch.save(out, sys.argv[2])
+"""
+
+
+def test_k32_ring_bitwise_equals_k64_double_buffer(gpu, tmp_path):
+    """The K32 ring (4/5 LDS stages of 32-deep K-steps) issues the same MFMAs in the same order as
+    the K64 double buffer (two K=32 MFMAs per 64-deep step), so forced-K32 and forced-K64 runs of
+    every tile must agree bit for bit -- outputs, BN partials and BN-backward sums."""
+    res = {}
+    for mode in ("0", "1"):
+        env = dict(os.environ, PDT_NT_K32=mode)
+        f = str(tmp_path / f"k32_{mode}.pt")
+        r = subprocess.run([sys.executable, "-c", _K32_SCRIPT, ROOT, f], env=env, capture_output=True,
+                           text=True, timeout=110)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res[mode] = torch.load(f, weights_only=True)
+    for key, a in res["0"].items():
+        for j, (u, v) in enumerate(zip(a, res["1"][key])):
+            assert torch.equal(u, v), (key, j)
