@@ -358,49 +358,48 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   // called for consecutive K-steps): no scalar divisions in the loop
   int k_ti = 0, k_tj = 0, k_chb = 0;
 
-  auto issue = [&](int kt, int buf) {
+  // One LDS-DMA wave instruction ("piece" q < A_PW + B_PW) of K-step kt into stage `buf`;
+  // `valid` false turns it into an all-OOB load (writes zeros, touches no memory).  C64: the
+  // tap / channel-block state (k_*) is that of step kt; advance() moves it on.  (Interleaving
+  // the pieces with the MFMAs instead of issuing a step's pieces as one burst was measured at
+  // -1% in-step, r2ac: profiles/r2_nt_mainloop_experiments.md.)
+  auto piece = [&](int kt, int buf, int q, bool valid) {
     char* As = smem + buf * CFG::STAGE_BYTES;
     char* Bs = As + BM * CFG::ROWB;
     if constexpr (C64) {
       const int tap = k_ti * P.tns + k_tj;
-      const int dr = P.dr0 + k_ti * P.dstep, ds = P.ds0 + k_tj * P.dstep;
-      const int tbo = ((P.tr0 + k_ti * P.tstep) * P.S + (P.ts0 + k_tj * P.tstep)) * P.CA + k_chb;
-      const int tdelta = ((dr * P.WA + ds) * P.CA + k_chb) * EB;
-#pragma unroll
-      for (int i = 0; i < A_PW; ++i) {
-        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[i], (unsigned)tap, 1u);
+      if (q < A_PW) {
+        const int i = q;
+        const int dr = P.dr0 + k_ti * P.dstep, ds = P.ds0 + k_tj * P.dstep;
+        const int tdelta = ((dr * P.WA + ds) * P.CA + k_chb) * EB;
+        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[i], (unsigned)tap, 1u) |
+                                (valid ? 0u : 0xffffffffu);
         const uint32_t off = (uint32_t)(a_base[i] + tdelta) | poison;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
-      }
-#pragma unroll
-      for (int i = 0; i < B_PW; ++i) {
-        uint32_t off = b_row[i] >= 0 ? (uint32_t)((b_row[i] + tbo) * EB + b_c[i] * 16) : OOB;
+      } else {
+        const int i = q - A_PW;
+        const int tbo = ((P.tr0 + k_ti * P.tstep) * P.S + (P.ts0 + k_tj * P.tstep)) * P.CA + k_chb;
+        uint32_t off = (valid && b_row[i] >= 0) ? (uint32_t)((b_row[i] + tbo) * EB + b_c[i] * 16) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
-      }
-      k_chb += KE;
-      if (k_chb == P.CA) {
-        k_chb = 0;
-        if (++k_tj == P.tns) { k_tj = 0; ++k_ti; }
       }
     } else if (P.c8) {
       // 8-channel source (the stem's super-pixel image): each 16-B chunk of a K-step is one
       // whole tap, tap = kt*8 + chunk, and the filter width divides 8, so a K-step advances
       // the source row by 8/S filter rows: offset = lane constant + kt * row step
-#pragma unroll
-      for (int i = 0; i < A_PW; ++i) {
+      if (q < A_PW) {
+        const int i = q;
         const int h = a_c8h[i] + kt * P.c8_rows;
         const bool ok = (unsigned)h < (unsigned)P.HA && a_c[i] < P.ntaps - kt * 8;
         glds16(ra, As + (wid * A_PW + i) * 1024, ok ? (uint32_t)(a_c8o[i] + kt * P.c8_step) : OOB);
-      }
-#pragma unroll
-      for (int i = 0; i < B_PW; ++i) {
+      } else {
+        const int i = q - A_PW;
         const int kk = kt * KE + b_c[i] * CE;
         uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * EB) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     } else {
-#pragma unroll
-      for (int i = 0; i < A_PW; ++i) {
+      if (q < A_PW) {
+        const int i = q;
         const int kk = kt * KE + a_c[i] * CE;
         const int tap = (int)fdiv((uint32_t)kk, P.div_ca);  // mul-hi, not a runtime divide
         const int ch = kk - tap * P.CA;
@@ -410,14 +409,27 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
         bool ok = kk < P.Kg && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
         uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * EB) : OOB;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
-      }
-#pragma unroll
-      for (int i = 0; i < B_PW; ++i) {
+      } else {
+        const int i = q - A_PW;
         const int kk = kt * KE + b_c[i] * CE;
         uint32_t off = (kk < P.Kg && b_row[i] >= 0) ? (uint32_t)((b_row[i] + kk) * EB) : OOB;
         glds16(rb, Bs + (wid * B_PW + i) * 1024, off);
       }
     }
+  };
+  auto advance = [&]() {
+    if constexpr (C64) {
+      k_chb += KE;
+      if (k_chb == P.CA) {
+        k_chb = 0;
+        if (++k_tj == P.tns) { k_tj = 0; ++k_ti; }
+      }
+    }
+  };
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int q = 0; q < A_PW + B_PW; ++q) piece(kt, buf, q, true);
+    advance();
   };
 
   const int wm = wid % WM, wn = wid / WM;

@@ -13,6 +13,7 @@
 #   prof[:args]            rocprofv3 --kernel-trace --stats of bench.py <args>  -> gpurun_out/TAG_prof
 #   pmc:<counters>[:args]  one rocprofv3 --pmc pass over bench.py <args>          -> gpurun_out/TAG_pmc_N
 #   py:<script>[:args]     python -u <script> <args>
+#   pmcpy:<ctrs>:<script>[:args]  one rocprofv3 --pmc pass over python <script> <args>  -> TAG_pmc_N
 #   env:VAR=VALUE          export VAR for the steps after it (env:VAR= unsets it)
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -59,6 +60,11 @@ for st in "$@"; do
       npmc=$((npmc+1))
       ( cd /tmp && export TMPDIR=/tmp && run "pmc_$npmc" 300 rocprofv3 --pmc ${ctr//+/ } --kernel-trace \
           --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/bench.py" $args ) || exit 1 ;;
+    pmcpy)
+      ctr=${rest%%:*}; r2=${rest#*:}; s=${r2%%:*}; args=""; [ "$s" != "$r2" ] && args=${r2#*:}; args=${args//,/ }
+      npmc=$((npmc+1))
+      ( cd /tmp && export TMPDIR=/tmp && run "pmc_$npmc" 300 rocprofv3 --pmc ${ctr//+/ } --kernel-trace \
+          --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/$s" $args ) || exit 1 ;;
     py)
       s=${rest%%:*}; args=""; [ "$s" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       run "py_$(basename "$s" .py)" 900 python -u "$s" $args || exit 1 ;;
