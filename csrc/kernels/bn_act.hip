@@ -12,8 +12,10 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <numeric>
 #include <stdexcept>
+#include <unordered_map>
 
 namespace pdt {
 
@@ -29,10 +31,24 @@ constexpr int FIN_GPB = FIN_ROWS * 16;      // groups per block (16 independent 
 
 // Per-channel-tile completion counters for the single-launch two-level reductions below
 // (zero-initialised once; the last block of a tile resets its counter, so launches on one stream
-// can reuse them back to back).  Forward finalize uses [0, 2048), backward reduce [2048, 4096);
-// two launches of the SAME reduction must not run concurrently on different streams.
+// can reuse them back to back).  One bank of kTileCounters per stream (counter_bank(): up to
+// kCounterBanks streams -- compute, capture, side, warm-up -- before banks are shared), so
+// reductions on different streams, e.g. a graph replay beside eager work, never share a counter.
+// Within a bank, forward finalize uses [0, 2048) and backward reduce [2048, 4096).
 constexpr int kTileCounters = 4096;
-__device__ unsigned int g_tile_counters[kTileCounters];
+constexpr int kCounterBanks = 8;
+__device__ unsigned int g_tile_counters[kCounterBanks * kTileCounters];
+
+static int counter_bank(hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, int> banks;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = banks.find(st);
+  if (it != banks.end()) return it->second * kTileCounters;
+  const int b = (int)(banks.size() % kCounterBanks);
+  banks.emplace(st, b);
+  return b * kTileCounters;
+}
 
 // PDT_BN_LASTBLOCK=0: two launches (partials, then finalize) instead of the last-block handshake
 static bool bn_lastblock() {
@@ -84,7 +100,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
                                                           const float* __restrict__ beta,
                                                           float momentum, float eps,
                                                           float* __restrict__ out, int mode,
-                                                          int nparts) {
+                                                          int nparts, int cbase) {
   // mode 0: partials + last-block finalize (one launch); 1: partials only; 2: finalize only
   __shared__ float sS[FIN_ROWS][FIN_CH + 1], sA[FIN_ROWS][FIN_CH + 1], sB[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
@@ -112,7 +128,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
     st_wt(o + k, S); st_wt(o + K + k, A); st_wt(o + 2 * K + k, B);
   }
   if (mode == 1) return;
-  if (!last_block_of_tile(blockIdx.x, gridDim.y)) return;
+  if (!last_block_of_tile(cbase + blockIdx.x, gridDim.y)) return;
   }
   const int P = mode == 2 ? nparts : gridDim.y;
   S = 0.f; A = 0.f; B = 0.f;
@@ -154,12 +170,13 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn_finalize: too many channels");
   if (bn_lastblock()) {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
-                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 0, P);
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 0, P,
+                       counter_bank(st));
   } else {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
-                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P);
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P, 0);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part,
-                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 2, P);
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 2, P, 0);
   }
 }
 
@@ -240,8 +257,9 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
   }
 }
 
-// grid of an 8-channel-vector elementwise pass: <= 8192 blocks of 256, rounded so that the grid
-// stride (blocks * 256) is a multiple of K8 -- every thread then keeps one channel group
+// grid of an 8-channel-vector elementwise pass: at most kEwCap (kEwCapResidual for the residual
+// apply) blocks of 256, rounded so that the grid stride (blocks * 256) is a multiple of K8 --
+// every thread then keeps one channel group
 static int ew_block_cap_env() {
   static int v = -1;
   if (v < 0) {
@@ -251,9 +269,10 @@ static int ew_block_cap_env() {
   return v;
 }
 
-// Grid caps measured per pass on MI355X (scripts/gpu_s5k.sh, 4096..32768): the residual-add
+// Grid caps measured per pass on MI355X (round-1 sweep of 4096..32768 blocks): the residual-add
 // forward apply (2 reads + 1 write + mask per vector) is fastest with one vector per thread
-// (cap 32768: 102 -> 94.5 us per call), the other passes with 8192.
+// (cap 32768: 102 -> 96.5 us per layer2 call), the other passes with 8192.  Capped multi-iteration
+// grids are checked against the default in tests/test_tiles_gpu.py (PDT_EW_BLOCKS=256).
 constexpr int kEwCap = 8192;
 constexpr int kEwCapResidual = 32768;
 
@@ -437,7 +456,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta, int mode,
-                                                          int nparts) {
+                                                          int nparts, int cbase) {
   __shared__ float sa[FIN_ROWS][FIN_CH + 1], sb[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
@@ -462,7 +481,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
     st_wt(o + K + k, b);
   }
   if (mode == 1) return;
-  if (!last_block_of_tile(kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
+  if (!last_block_of_tile(cbase + kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
   }
   const int P = mode == 2 ? nparts : gridDim.y;
   a = 0.f; b = 0.f;
@@ -637,12 +656,12 @@ void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn reduce: too many channels");
   if (bn_lastblock()) {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 0, P);
+                       sums, invstd, dgamma, dbeta, 0, P, counter_bank(st));
   } else {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 1, P);
+                       sums, invstd, dgamma, dbeta, 1, P, 0);
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 2, P);
+                       sums, invstd, dgamma, dbeta, 2, P, 0);
   }
 }
 

@@ -332,3 +332,33 @@ def test_k32_ring_bitwise_equals_k64_double_buffer(gpu, tmp_path):
     for key, a in res["0"].items():
         for j, (u, v) in enumerate(zip(a, res["1"][key])):
             assert torch.equal(u, v), (key, j)
+
+
+def test_bn_reductions_concurrent_on_two_streams(gpu, native_ext):
+    """The single-launch BN reductions count finished blocks per channel tile; each stream gets
+    its own counter bank, so the same reduction racing on two streams (a graph replay beside
+    eager work, the warm-up stream of a capture) must give the single-stream result every time."""
+    C = native_ext
+    k, grows, ng = 256, 256, 3136
+    g = torch.Generator().manual_seed(7)
+    y = torch.randn(ng, grows, k, generator=g)
+    part = torch.stack([y.sum(1), ((y - y.mean(1, keepdim=True)) ** 2).sum(1)], 1).contiguous().to(gpu)
+    ones, zeros = torch.ones(k, device=gpu), torch.zeros(k, device=gpu)
+
+    def fin():
+        return C.bn_finalize(part, ng * grows, zeros.clone(), ones.clone(), ones, zeros, 0.1, 1e-5)
+
+    ref_stats = fin()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(16):
+        s1.wait_stream(torch.cuda.current_stream())
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s1):
+            outs.append(fin())
+        with torch.cuda.stream(s2):
+            outs.append(fin())
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref_stats)
