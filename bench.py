@@ -118,8 +118,8 @@ def main(argv=None) -> int:
         set_random_seeds(0, deterministic=True)
 
     if args.fp8:
-        if args.impl != "native" or args.graph:
-            raise SystemExit("--fp8 needs --impl native and no --graph (delayed scaling slots advance per call)")
+        if args.impl != "native":
+            raise SystemExit("--fp8 needs --impl native")
         ops.set_fp8(True)
     if args.impl == "native":
         model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
@@ -170,7 +170,10 @@ def main(argv=None) -> int:
     if args.graph:
         from pytorch_distributed_tutorials_amd.utils.graph import CapturedStep
         eager_step = step
-        step = CapturedStep(eager_step, warmup=max(1, min(args.warmup, 3)))
+        # fp8: three graphs, one per phase of the delayed-scaling slot ring (utils/graph.py)
+        from pytorch_distributed_tutorials_amd.ops.fused import FP8_RING
+        step = CapturedStep(eager_step, warmup=max(1, min(args.warmup, 3)), period=3 if args.fp8 else 1,
+                            ring=FP8_RING if args.fp8 else None)
 
     def barrier():
         if world > 1:

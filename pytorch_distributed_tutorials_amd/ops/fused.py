@@ -16,6 +16,7 @@ dgrad and wgrad implicit GEMMs.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -51,16 +52,20 @@ def fp8_enabled() -> bool:
     return _FP8
 
 
+_Q8_STATES: list = []  # weak references to every _Q8State, creation order (fp8_phase_signature)
+
+
 class _Q8State:
     """Delayed-scaling state of one fp8 activation producer (csrc/kernels/fp8.hip contract)."""
 
-    __slots__ = ("buf", "t", "off")
+    __slots__ = ("buf", "t", "off", "__weakref__")
 
     def __init__(self, device):
         C = native()
         self.buf = torch.zeros(C.fp8_state_floats(), dtype=torch.float32, device=device)
         self.off = C.fp8_deq_offset()
         self.t = 0
+        _Q8_STATES.append(weakref.ref(self))
 
     def next_slot(self) -> int:
         slot = self.t % 3
@@ -69,6 +74,23 @@ class _Q8State:
 
     def deq(self, slot: int) -> torch.Tensor:
         return self.buf.narrow(0, self.off + slot, 1)
+
+
+def fp8_ring_state() -> tuple:
+    """Step counter of every live delayed-scaling slot ring (creation order): the host state a
+    captured fp8 step bakes in (utils.graph.CapturedStep ``ring``)."""
+    _Q8_STATES[:] = [r for r in _Q8_STATES if r() is not None]
+    return tuple(r().t for r in _Q8_STATES)
+
+
+def fp8_set_ring_state(ts: tuple) -> None:
+    """Set the step counters read by fp8_ring_state (same order)."""
+    live = [r() for r in _Q8_STATES if r() is not None]
+    for st, t in zip(live, ts):
+        st.t = t
+
+
+FP8_RING = (fp8_ring_state, fp8_set_ring_state)
 
 
 def _q8_state(owner, device, attr: str = "_pdt_q8") -> _Q8State:

@@ -191,12 +191,16 @@ class WeightMirror:
         }
 
     def ensure_fp8(self) -> bool:
-        """Quantize both bf16 images to e4m3 (one launch each) if they changed since last time."""
+        """Quantize both bf16 images to e4m3 (one launch each) if they changed since last time.
+        Under graph capture the launches are always recorded: a replayed step cannot consult the
+        host key, and the weights it sees were changed by the previous replay's optimizer step
+        (an eager forward just before capture -- an evaluation -- would otherwise leave the
+        first captured step without its quantization)."""
         if not self.valid() or not self._tracked:
             return False
         if self._fp8 is None:
             self._build_fp8()
-        if self.key8 != self.key:
+        if self.key8 != self.key or torch.cuda.is_current_stream_capturing():
             from ..ops._ext import native
             C, f = native(), self._fp8
             C.quant_rows_e4m3(self.krsc, f["krsc8"], f["kscale"], f["tk"], f["mk"])

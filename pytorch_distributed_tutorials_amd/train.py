@@ -111,12 +111,19 @@ class _GraphStep:
 
     WARMUP = 3
 
-    def __init__(self, ddp_model, criterion, optimizer):
+    def __init__(self, ddp_model, criterion, optimizer, period: int = 1):
         self.ddp_model, self.criterion, self.optimizer = ddp_model, criterion, optimizer
+        self.period = period  # 3 with fp8: the delayed-scaling slot ring (utils.graph.CapturedStep)
         self.x = self.y = None
         self.warm = 0
         self.side = None
         self.captured = None
+        self.hyper = None
+
+    def _hyperparameters(self):
+        """The optimizer settings the fused SGD launch bakes into the graph as kernel arguments."""
+        return [tuple((k, v) for k, v in sorted(g.items()) if k != "params" and isinstance(v, (int, float, bool)))
+                for g in self.optimizer.param_groups]
 
     def eager(self, inputs, labels):
         self.optimizer.zero_grad()
@@ -145,8 +152,17 @@ class _GraphStep:
             return loss
         self.x.copy_(inputs)
         self.y.copy_(labels)
+        hyper = self._hyperparameters()
+        if self.captured is not None and (hyper != self.hyper or not self.captured.in_phase()):
+            # lr / momentum / weight decay changed (a scheduler, user code): the captured SGD
+            # launch would keep the old values; or (fp8) an eager partial batch / an evaluation
+            # advanced the delayed-scaling slot rings past the graphs' phases -- capture again
+            self.captured = None
         if self.captured is None:
-            self.captured = CapturedStep(lambda: self.eager(self.x, self.y), warmup=0)
+            from .ops.fused import FP8_RING
+            self.hyper = hyper
+            self.captured = CapturedStep(lambda: self.eager(self.x, self.y), warmup=0, period=self.period,
+                                         ring=FP8_RING if self.period > 1 else None)
         return self.captured()
 
 
@@ -182,8 +198,6 @@ def main(argv: Optional[list] = None) -> int:
     if dtype == "fp8":
         if impl != "native" or device.type != "cuda":
             raise SystemExit("--dtype fp8 needs the native impl on a GPU")
-        if args.graph:
-            raise SystemExit("--graph with --dtype fp8: the delayed-scaling slots advance per call")
         ops.set_fp8(True)
     if args.graph and (impl != "native" or device.type != "cuda"):
         raise SystemExit("--graph needs the native impl on a GPU")
@@ -227,7 +241,8 @@ def main(argv: Optional[list] = None) -> int:
                                 device=device, seed=args.seed + env.rank)
     test_loader = DeviceLoader(test_set, 128, shuffle=False, augment=False, device=device)
 
-    graph_step = _GraphStep(ddp_model, criterion, optimizer) if args.graph else None
+    graph_step = _GraphStep(ddp_model, criterion, optimizer, period=3 if dtype == "fp8" else 1) \
+        if args.graph else None
     global_step = 0
     done = False
     for epoch in range(start_epoch, args.num_epochs):

@@ -17,19 +17,52 @@ the ResNet graph is static (same shapes, same buckets, every step).
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Callable, List, Optional, Tuple
 
 import torch
 
 
 class CapturedStep:
+    """Capture ``step_fn`` once (after ``warmup`` eager calls on a side stream) and replay it.
+
+    ``period`` > 1 captures that many consecutive steps as separate graphs (sharing one memory
+    pool) and replays them round-robin.  That keeps host-side state that cycles with the step
+    count valid under replay: fp8 delayed scaling rotates a 3-slot amax/scale ring per step
+    (``ops.fused._Q8State``), so graph k bakes in the slot indices of a step t = t0 + k.
+
+    ``ring = (get, set)`` exposes that host state (a tuple of step counters).  Capture executes
+    nothing on the device, so after capturing, the counters are put back to their pre-capture
+    values and every replay advances them by one step's worth -- the host always describes what
+    the device has run, and eager work between replays (an evaluation, a partial batch) uses
+    the right slots.  ``in_phase()`` tells whether the next replay's baked-in slots still match
+    the counters (eager work that advanced a ring by other than a multiple of its cycle breaks
+    them: capture again).
+    """
+
     def __init__(self, step_fn: Callable[[], torch.Tensor], warmup: int = 3,
-                 pool: Optional[tuple] = None):
+                 pool: Optional[tuple] = None, period: int = 1,
+                 ring: Optional[Tuple[Callable[[], Tuple[int, ...]], Callable[[Tuple[int, ...]], None]]] = None,
+                 cycle: int = 3):
+        if period < 1:
+            raise ValueError("period must be >= 1")
         self.step_fn = step_fn
         self.warmup = warmup
         self.pool = pool
-        self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.output: Optional[torch.Tensor] = None
+        self.period = period
+        self.ring = ring
+        self.cycle = cycle
+        self.phase_sig: List[Tuple[int, ...]] = []  # counters (mod cycle) graph k was captured at
+        self.delta: Tuple[int, ...] = ()            # counter advance of one step
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.outputs: List[torch.Tensor] = []
+        self.calls = 0
+
+    @property
+    def graph(self) -> Optional[torch.cuda.CUDAGraph]:
+        return self.graphs[0] if self.graphs else None
+
+    def _mod(self, t: Tuple[int, ...]) -> Tuple[int, ...]:
+        return tuple(v % self.cycle for v in t)
 
     def capture(self) -> None:
         # warm up on a side stream (lazy init, allocator pools, kernel attributes), then capture
@@ -40,13 +73,39 @@ class CapturedStep:
                 self.step_fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=self.pool):
-            self.output = self.step_fn()
+        start = self.ring[0]() if self.ring is not None else ()
+        pool = self.pool
+        for _ in range(self.period):
+            if self.ring is not None:
+                self.phase_sig.append(self._mod(self.ring[0]()))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                out = self.step_fn()
+            if pool is None:
+                pool = g.pool()  # later phases reuse the first graph's private pool
+            self.graphs.append(g)
+            self.outputs.append(out)
+        if self.ring is not None:
+            end = self.ring[0]()
+            if len(end) != len(start):
+                raise RuntimeError("CapturedStep: the captured step created new ring state; warm it up first")
+            self.delta = tuple((e - b) // self.period for b, e in zip(start, end))
+            self.ring[1](start)  # the device has run none of the captured steps yet
         torch.cuda.synchronize()
 
+    def in_phase(self) -> bool:
+        """False when eager work moved the host counters off the next replay's baked-in phase."""
+        if not self.graphs or self.ring is None:
+            return True
+        cur = self.ring[0]()
+        return len(cur) == len(self.delta) and self._mod(cur) == self.phase_sig[self.calls % self.period]
+
     def __call__(self) -> torch.Tensor:
-        if self.graph is None:
+        if not self.graphs:
             self.capture()
-        self.graph.replay()
-        return self.output
+        k = self.calls % self.period
+        self.calls += 1
+        self.graphs[k].replay()
+        if self.ring is not None:
+            self.ring[1](tuple(t + d for t, d in zip(self.ring[0](), self.delta)))
+        return self.outputs[k]

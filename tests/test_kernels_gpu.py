@@ -536,21 +536,27 @@ def test_stem_superpixel_matches_generic(gpu, native_ext):
     assert _rel_err(bn.bias.grad, bn2.bias.grad) < 2e-2
 
 
-def test_captured_step_matches_eager(gpu, native_ext):
+@pytest.mark.parametrize("arch,fp8", [("resnet18", False), ("resnet50", False), ("resnet18", True)])
+def test_captured_step_matches_eager(gpu, native_ext, arch, fp8):
     """A training step captured in a HIP graph and replayed == the same steps run eagerly
-    (deterministic kernels: bitwise), including the fused SGD and the weight mirror."""
+    (deterministic kernels: bitwise), including the fused SGD and the weight mirror.  fp8: the
+    delayed-scaling slot ring cycles every 3 steps, so the step is captured as 3 graphs replayed
+    round-robin (CapturedStep period=3); 5 replays cover a full cycle and a wrap."""
     import copy
     from pytorch_distributed_tutorials_amd import ops
     from pytorch_distributed_tutorials_amd.models import build_model
     from pytorch_distributed_tutorials_amd.optim import SGD
     from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
     from pytorch_distributed_tutorials_amd.utils import seed as seedmod
+    from pytorch_distributed_tutorials_amd.ops.fused import FP8_RING
     from pytorch_distributed_tutorials_amd.utils.graph import CapturedStep
     old = seedmod._DETERMINISTIC
     seedmod._DETERMINISTIC = True
+    old_fp8 = ops.fp8_enabled()
+    ops.set_fp8(fp8)
     try:
         torch.manual_seed(0)
-        base = build_model("resnet18", num_classes=10).to(gpu).set_impl("native")
+        base = build_model(arch, num_classes=10).to(gpu).set_impl("native")
         x = torch.randn(32, 3, 32, 32, device=gpu)
         y = torch.randint(0, 10, (32,), device=gpu)
         runs = []
@@ -567,8 +573,9 @@ def test_captured_step_matches_eager(gpu, native_ext):
                 return loss
             for _ in range(2):
                 step()
-            run = CapturedStep(step, warmup=0) if graphed else step
-            losses = [float(run()) for _ in range(3)]
+            run = CapturedStep(step, warmup=0, period=3 if fp8 else 1,
+                               ring=FP8_RING if fp8 else None) if graphed else step
+            losses = [float(run()) for _ in range(5 if fp8 else 3)]
             runs.append((losses, [p.detach().clone() for p in m.parameters()]))
         (l0, p0), (l1, p1) = runs
         assert l0 == l1, (l0, l1)
@@ -576,6 +583,70 @@ def test_captured_step_matches_eager(gpu, native_ext):
             assert torch.equal(a, b)
     finally:
         seedmod._DETERMINISTIC = old
+        ops.set_fp8(old_fp8)
+
+
+@pytest.mark.parametrize("n_eval", [1, 3])
+def test_captured_fp8_step_with_evaluation_between_replays(gpu, native_ext, n_eval):
+    """fp8 under graph replay with eager work in between: an evaluation advances the forward
+    slot rings by n_eval steps.  The host ring counters follow the replays (CapturedStep ring),
+    so the evaluation uses the slots the device expects; n_eval = 1 leaves the graphs out of phase
+    (in_phase() False -> capture again, whose first step must still quantize the weights the
+    evaluation already saw), n_eval = 3 keeps them in phase.  Bitwise equal to eager."""
+    import copy
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.ops.fused import FP8_RING
+    from pytorch_distributed_tutorials_amd.optim import SGD
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_tutorials_amd.utils import seed as seedmod
+    from pytorch_distributed_tutorials_amd.utils.graph import CapturedStep
+    old, old_fp8 = seedmod._DETERMINISTIC, ops.fp8_enabled()
+    seedmod._DETERMINISTIC = True
+    ops.set_fp8(True)
+    try:
+        torch.manual_seed(0)
+        base = build_model("resnet18", num_classes=10).to(gpu).set_impl("native")
+        x = torch.randn(32, 3, 32, 32, device=gpu)
+        y = torch.randint(0, 10, (32,), device=gpu)
+        xe = torch.randn(32, 3, 32, 32, device=gpu)
+        runs = []
+        for graphed in (False, True):
+            m = copy.deepcopy(base)
+            ddp = DistributedDataParallel(m)
+            opt = SGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+
+            def step():
+                opt.zero_grad()
+                loss = ops.cross_entropy(ddp(x), y)
+                loss.backward()
+                opt.step()
+                return loss
+            for _ in range(2):
+                step()
+            mk = lambda: CapturedStep(step, warmup=0, period=3, ring=FP8_RING)  # noqa: E731
+            run = mk() if graphed else step
+            losses, recaptures = [], 0
+            for i in range(8):
+                if i == 4:
+                    m.eval()
+                    with torch.no_grad():
+                        for _ in range(n_eval):
+                            ddp(xe)
+                    m.train()
+                if graphed and not run.in_phase():
+                    run = mk()
+                    recaptures += 1
+                losses.append(float(run().detach()))
+            runs.append((losses, [p.detach().clone() for p in m.parameters()], recaptures))
+        (l0, p0, _), (l1, p1, rc) = runs
+        assert rc == (1 if n_eval % 3 else 0)
+        assert l0 == l1, (l0, l1)
+        for a, b in zip(p0, p1):
+            assert torch.equal(a, b)
+    finally:
+        seedmod._DETERMINISTIC = old
+        ops.set_fp8(old_fp8)
 
 
 @pytest.mark.parametrize("deterministic", [True, False])
@@ -647,23 +718,58 @@ def test_relu_bitmask_dgrad_matches_z_mask(gpu, native_ext):
     assert torch.equal(s1, s3)
 
 
-def test_trainer_graph_matches_eager(gpu, native_ext, tmp_path):
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_trainer_graph_matches_eager(gpu, native_ext, tmp_path, dtype):
     """train.py --graph (HIP-graph replay of the whole step, eager warm-up and partial batches)
     trains every batch exactly once: same weights as the eager trainer, bit for bit (the default
     deterministic kernels), across an epoch boundary with a partial last batch and an evaluation.
     The checkpoint is written at the start of each epoch, so the one of epoch 2 holds the state
-    after epochs 0 and 1."""
+    after epochs 0 and 1.  fp8: three graphs, one per delayed-scaling slot phase."""
+    from pytorch_distributed_tutorials_amd import ops
     from pytorch_distributed_tutorials_amd.train import main
     base = ["--arch", "resnet18", "--data", "synthetic-cifar", "--synthetic-samples", "200",
-            "--batch-size", "32", "--num_epochs", "3", "--eval-every", "1", "--num-classes", "10"]
+            "--batch-size", "32", "--num_epochs", "3", "--eval-every", "1", "--num-classes", "10",
+            "--dtype", dtype]
+    old_fp8 = ops.fp8_enabled()
     sds = []
-    for extra, sub in (([], "eager"), (["--graph"], "graph")):
-        d = tmp_path / sub
-        assert main(base + extra + ["--model_dir", str(d)]) == 0
-        sds.append(torch.load(d / "resnet_distributed.pth", weights_only=True))
+    try:
+        for extra, sub in (([], "eager"), (["--graph"], "graph")):
+            d = tmp_path / sub
+            assert main(base + extra + ["--model_dir", str(d)]) == 0
+            sds.append(torch.load(d / "resnet_distributed.pth", weights_only=True))
+    finally:
+        ops.set_fp8(old_fp8)
     assert sds[0].keys() == sds[1].keys()
     for k in sds[0]:
         assert torch.equal(sds[0][k], sds[1][k]), k
+
+
+def test_graph_step_recaptures_on_hyperparameter_change(gpu, native_ext):
+    """The captured fused-SGD launch bakes lr / momentum / weight decay in as kernel arguments:
+    a changed param group must trigger a fresh capture, never a stale replay."""
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.optim import SGD
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_tutorials_amd.train import _GraphStep
+    torch.manual_seed(0)
+    m = build_model("resnet18", num_classes=10).to(gpu).set_impl("native")
+    ddp = DistributedDataParallel(m)
+    opt = SGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    gs = _GraphStep(ddp, ops.cross_entropy, opt)
+    x = torch.randn(16, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (16,), device=gpu)
+    for _ in range(gs.WARMUP + 2):
+        gs(x, y)
+    first = gs.captured
+    assert first is not None and first.calls == 2
+    gs(x, y)
+    assert gs.captured is first  # unchanged hyperparameters: replay
+    for g in opt.param_groups:
+        g["lr"] = 0.01
+    gs(x, y)
+    assert gs.captured is not first and gs.captured.calls == 1
+    assert dict(gs.hyper[0])["lr"] == 0.01
 
 
 @pytest.mark.parametrize("mask", [False, True])
