@@ -54,17 +54,20 @@ for st in "$@"; do
     prof)
       args=${rest//,/ }
       ( cd /tmp && export TMPDIR=/tmp && run prof 500 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$O/${TAG}_prof" -o run -- python3 "$R/bench.py" $args ) || exit 1 ;;
+          -d "$O/${TAG}_prof" -o run -- python3 "$R/bench.py" $args ) || exit 1
+      nstep=$((nstep+1)) ;;  # run() counted inside the subshell
     pmc)
       ctr=${rest%%:*}; args=""; [ "$ctr" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       npmc=$((npmc+1))
       ( cd /tmp && export TMPDIR=/tmp && run "pmc_$npmc" 300 rocprofv3 --pmc ${ctr//+/ } --kernel-trace \
-          --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/bench.py" $args ) || exit 1 ;;
+          --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/bench.py" $args ) || exit 1
+      nstep=$((nstep+1)) ;;  # run() counted inside the subshell
     pmcpy)
       ctr=${rest%%:*}; r2=${rest#*:}; s=${r2%%:*}; args=""; [ "$s" != "$r2" ] && args=${r2#*:}; args=${args//,/ }
       npmc=$((npmc+1))
       ( cd /tmp && export TMPDIR=/tmp && run "pmc_$npmc" 300 rocprofv3 --pmc ${ctr//+/ } --kernel-trace \
-          --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/$s" $args ) || exit 1 ;;
+          --output-format csv -d "$O/${TAG}_pmc_$npmc" -o run -- python3 "$R/$s" $args ) || exit 1
+      nstep=$((nstep+1)) ;;
     py)
       s=${rest%%:*}; args=""; [ "$s" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       run "py_$(basename "$s" .py)" 900 python -u "$s" $args || exit 1 ;;

@@ -1,0 +1,40 @@
+"""Per-step kernel time by stream and kernel family from a rocprofv3 kernel trace (the last full
+step between two optimizer launches): python scripts/trace_breakdown.py run_kernel_trace.csv"""
+import collections
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+a, b = idx[-2], idx[-1]
+step = rows[a + 1:b + 1]
+t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
+print(f"step span {(t1 - t0) / 1000:.1f} us, {len(step)} kernels")
+
+
+def family(n):
+    n = n.split("(")[0].replace("void ", "").replace("pdt::", "")
+    for key in ("igemm_nt_kernel", "igemm_tn_kernel", "bn_bwd_apply", "bn_act_fwd", "bn_finalize",
+                "bn_bwd_part", "bn_bwd_reduce", "quant", "pool_bn", "fc_gemm", "sgd", "pack"):
+        if key in n:
+            if key == "igemm_nt_kernel":
+                args = n.split("<")[1].split(">")[0].split(",")
+                op = args[7].strip() if len(args) > 7 else "0"
+                epi = args[6].strip()
+                return f"nt epi{epi} op{op}"
+            return key
+    return n[:40]
+
+
+by = collections.defaultdict(lambda: [0, 0.0])
+for r in step:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+    k = (r["Stream_Id"], family(r["Kernel_Name"]))
+    by[k][0] += 1
+    by[k][1] += d
+tot = collections.defaultdict(float)
+for (s, n), (c, d) in sorted(by.items(), key=lambda x: -x[1][1]):
+    tot[s] += d
+    print(f"stream {s:>2} {c:4d} calls {d:9.1f} us  {n}")
+print({k: round(v, 1) for k, v in tot.items()})
