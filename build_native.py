@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Build the native extension in-tree for gfx950 (MI355X).
 
-    python build_native.py [--force] [--jobs N] [--debug]
+    python build_native.py [--force] [--jobs N] [--debug] [--sanitize]
 
 * every ``csrc/kernels/*.hip`` is compiled by ``hipcc --offload-arch=gfx950``
   WITHOUT PyTorch headers (fast, seconds per file);
@@ -12,6 +12,12 @@
 
 Incremental: an object is rebuilt when its source or any header under csrc/ is
 newer.  Works without a GPU (hipcc cross-compiles), so it runs in CI/CPU boxes.
+
+``--sanitize``: a host-side AddressSanitizer + UndefinedBehaviorSanitizer build (``-O1 -g``,
+``-fsanitize=address,undefined`` on the host compilation only -- GPU code stays uninstrumented)
+into ``build/asan/_C*.so``, for the CPU tests of the host runtime (C++ reducer, bucket plan,
+bindings' argument checks).  Run them with ``scripts/asan_cpu_tests.sh``: it preloads the clang
+ASan runtime into python and points the loader at this build (``PDT_NATIVE_SO``).
 """
 from __future__ import annotations
 
@@ -55,10 +61,20 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = True) -> str:
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+
+
+def asan_out_path() -> str:
+    return os.path.join(ROOT, "build", "asan", "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = True,
+          sanitize: bool = False) -> str:
     tdir, tinc, abi = _torch_paths()
-    os.makedirs(BUILD, exist_ok=True)
-    opt = ["-O0", "-g"] if debug else ["-O3"]
+    bdir = os.path.join(ROOT, "build", "native_asan") if sanitize else BUILD
+    os.makedirs(bdir, exist_ok=True)
+    opt = ["-O0", "-g"] if debug else (["-O1", "-g"] + SAN_FLAGS if sanitize else ["-O3"])
     common = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
               "-Wno-unused-result", "-Wno-unused-value"] + opt
     kern_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
@@ -73,7 +89,7 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
     objs = []
     for src in kern_srcs + host_srcs:
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-        obj = os.path.join(BUILD, rel + ".o")
+        obj = os.path.join(bdir, rel + ".o")
         objs.append(obj)
         stale = force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)
         if not stale:
@@ -93,12 +109,15 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
                 f.result()
                 if verbose:
                     print(f"[build_native]   ok {os.path.relpath(futs[f], ROOT)}", flush=True)
-    so = out_path()
+    so = asan_out_path() if sanitize else out_path()
+    os.makedirs(os.path.dirname(so), exist_ok=True)
     if force or jobs_list or not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(o) for o in objs):
         tlib = os.path.join(tdir, "lib")
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", so] + objs + [
             "-L", tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             os.path.join(tlib, "librccl.so"), f"-Wl,-rpath,{tlib}", "-Wl,-rpath,/opt/rocm/lib"]
+        if sanitize:
+            link += ["-fsanitize=address,undefined", "-shared-libsan"]
         _run(link)
         if verbose:
             print(f"[build_native] linked {os.path.relpath(so, ROOT)}", flush=True)
@@ -114,8 +133,9 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="host ASan+UBSan build into build/asan/")
     a = ap.parse_args(argv)
-    so = build(force=a.force, jobs=a.jobs, debug=a.debug)
+    so = build(force=a.force, jobs=a.jobs, debug=a.debug, sanitize=a.sanitize)
     print(so)
     return 0
 

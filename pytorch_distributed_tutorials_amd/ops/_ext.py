@@ -27,6 +27,15 @@ def _load() -> None:
         return
     try:
         import torch  # noqa: F401  (libtorch must be loaded before _C)
+        so = os.environ.get("PDT_NATIVE_SO")
+        if so:  # an alternative build of the same module (build_native.py --sanitize)
+            import importlib.util
+            import sys
+            spec = importlib.util.spec_from_file_location("pytorch_distributed_tutorials_amd._C", so)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["pytorch_distributed_tutorials_amd._C"] = _C
+            return
         _C = importlib.import_module("pytorch_distributed_tutorials_amd._C")
     except BaseException as e:  # ImportError, OSError (missing .so deps) ...
         _C = None
