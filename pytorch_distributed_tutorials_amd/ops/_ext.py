@@ -9,6 +9,7 @@ device tensors.  CPU tensors use the PyTorch reference implementations (tests).
 from __future__ import annotations
 
 import importlib
+import importlib.util as importlib_util
 import os
 from typing import Any, Optional
 
@@ -29,10 +30,9 @@ def _load() -> None:
         import torch  # noqa: F401  (libtorch must be loaded before _C)
         so = os.environ.get("PDT_NATIVE_SO")
         if so:  # an alternative build of the same module (build_native.py --sanitize)
-            import importlib.util
             import sys
-            spec = importlib.util.spec_from_file_location("pytorch_distributed_tutorials_amd._C", so)
-            _C = importlib.util.module_from_spec(spec)
+            spec = importlib_util.spec_from_file_location("pytorch_distributed_tutorials_amd._C", so)
+            _C = importlib_util.module_from_spec(spec)
             spec.loader.exec_module(_C)
             sys.modules["pytorch_distributed_tutorials_amd._C"] = _C
             return
