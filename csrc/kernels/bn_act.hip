@@ -28,6 +28,19 @@ namespace pdt {
 constexpr int FIN_CH = 32;
 constexpr int FIN_ROWS = 8;                 // threads per channel in a block
 constexpr int FIN_GPB = FIN_ROWS * 16;      // groups per block (16 independent loads per thread)
+// Up to FIN_SINGLE groups, ONE block per 32-channel tile reads them all and finishes in place:
+// no partial round trip and no last-block handshake (a dependent sc1 store / atomic / sc1 load
+// chain worth ~2-3 us of a ~6 us launch; every ResNet-50 layer2-4 BN qualifies).
+constexpr int FIN_SINGLE = 512;
+static int fin_single() {  // PDT_FIN_SINGLE=0: always two-level (A/B knob)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_FIN_SINGLE");
+    v = e ? std::max(0, atoi(e)) : FIN_SINGLE;
+  }
+  return v;
+}
+static int fin_gpb(int G) { return G <= fin_single() ? std::max(G, 1) : FIN_GPB; }
 
 // Per-channel-tile completion counters for the single-launch two-level reductions below
 // (zero-initialised once; the last block of a tile resets its counter, so launches on one stream
@@ -100,13 +113,13 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
                                                           const float* __restrict__ beta,
                                                           float momentum, float eps,
                                                           float* __restrict__ out, int mode,
-                                                          int nparts, int cbase) {
+                                                          int nparts, int cbase, int gpb) {
   // mode 0: partials + last-block finalize (one launch); 1: partials only; 2: finalize only
   __shared__ float sS[FIN_ROWS][FIN_CH + 1], sA[FIN_ROWS][FIN_CH + 1], sB[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
-  const int g0 = blockIdx.y * FIN_GPB;
-  const int g1 = min(ngroups, g0 + FIN_GPB);
+  const int g0 = blockIdx.y * gpb;
+  const int g1 = min(ngroups, g0 + gpb);
   float S = 0.f, A = 0.f, B = 0.f;
   if (mode != 2) {
   if (k < K) {
@@ -122,15 +135,24 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   }
   sS[ty][tx] = S; sA[ty][tx] = A; sB[ty][tx] = B;
   __syncthreads();
+  const bool direct = mode == 0 && gridDim.y == 1;  // one partition: finish in place
   if (ty == 0 && k < K) {
     for (int r = 1; r < FIN_ROWS; ++r) { S += sS[r][tx]; A += sA[r][tx]; B += sB[r][tx]; }
-    float* o = ws + ((int64_t)blockIdx.y * 3) * K;
-    st_wt(o + k, S); st_wt(o + K + k, A); st_wt(o + 2 * K + k, B);
+    if (!direct) {
+      float* o = ws + ((int64_t)blockIdx.y * 3) * K;
+      st_wt(o + k, S); st_wt(o + K + k, A); st_wt(o + 2 * K + k, B);
+    }
   }
   if (mode == 1) return;
-  if (!last_block_of_tile(cbase + blockIdx.x, gridDim.y)) return;
+  if (direct) {
+    if (ty != 0 || k >= K) return;
+  } else if (!last_block_of_tile(cbase + blockIdx.x, gridDim.y)) {
+    return;
   }
+  }
+  const bool direct = mode == 0 && gridDim.y == 1;
   const int P = mode == 2 ? nparts : gridDim.y;
+  if (!direct) {
   S = 0.f; A = 0.f; B = 0.f;
   if (k < K) {
 #pragma unroll 8
@@ -143,6 +165,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   __syncthreads();
   if (ty != 0 || k >= K) return;
   for (int r = 1; r < FIN_ROWS; ++r) { S += sS[r][tx]; A += sA[r][tx]; B += sB[r][tx]; }
+  }
   const float mu = S / (float)M;
   const float m2 = fmaxf(A + B - S * mu, 0.f);
   const float var = m2 / (float)M;
@@ -159,24 +182,25 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   out[3 * K + k] = beta[k] - mu * sc;
 }
 
-int bn_finalize_partitions(int ngroups) { return ceil_div(ngroups, FIN_GPB); }
+int bn_finalize_partitions(int ngroups) { return ceil_div(ngroups, fin_gpb(ngroups)); }
 
 void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K, float* rm, float* rv,
                         const float* gamma, const float* beta, float momentum, float eps,
                         float* out, hipStream_t st) {
   // workspace for stage-1 partials lives after out[4][K] (caller allocates 4K + 3K*P floats)
-  int P = ceil_div(ngroups, FIN_GPB);
+  const int gpb = fin_gpb(ngroups);
+  int P = ceil_div(ngroups, gpb);
   float* ws = out + 4 * (int64_t)K;
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn_finalize: too many channels");
   if (bn_lastblock()) {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
                        ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 0, P,
-                       counter_bank(st));
+                       P > 1 ? counter_bank(st) : 0, gpb);
   } else {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
-                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P, 0);
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P, 0, gpb);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part,
-                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 2, P, 0);
+                       ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 2, P, 0, gpb);
   }
 }
 
@@ -456,12 +480,12 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
                                                           const float* __restrict__ invstd,
                                                           float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta, int mode,
-                                                          int nparts, int cbase) {
+                                                          int nparts, int cbase, int gpb) {
   __shared__ float sa[FIN_ROWS][FIN_CH + 1], sb[FIN_ROWS][FIN_CH + 1];
   const int tx = threadIdx.x & (FIN_CH - 1), ty = threadIdx.x / FIN_CH;
   const int k = blockIdx.x * FIN_CH + tx;
-  const int g0 = blockIdx.y * FIN_GPB;
-  const int g1 = min(G, g0 + FIN_GPB);
+  const int g0 = blockIdx.y * gpb;
+  const int g1 = min(G, g0 + gpb);
   float a = 0.f, b = 0.f;
   if (mode != 2) {
   if (k < K) {
@@ -474,16 +498,25 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   sa[ty][tx] = a;
   sb[ty][tx] = b;
   __syncthreads();
+  const bool direct = mode == 0 && gridDim.y == 1;  // one partition: finish in place
   if (ty == 0 && k < K) {
     for (int r = 1; r < FIN_ROWS; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
-    float* o = ws + (int64_t)blockIdx.y * 2 * K;
-    st_wt(o + k, a);
-    st_wt(o + K + k, b);
+    if (!direct) {
+      float* o = ws + (int64_t)blockIdx.y * 2 * K;
+      st_wt(o + k, a);
+      st_wt(o + K + k, b);
+    }
   }
   if (mode == 1) return;
-  if (!last_block_of_tile(cbase + kTileCounters / 2 + blockIdx.x, gridDim.y)) return;
+  if (direct) {
+    if (ty != 0 || k >= K) return;
+  } else if (!last_block_of_tile(cbase + kTileCounters / 2 + blockIdx.x, gridDim.y)) {
+    return;
   }
+  }
+  const bool direct = mode == 0 && gridDim.y == 1;
   const int P = mode == 2 ? nparts : gridDim.y;
+  if (!direct) {
   a = 0.f; b = 0.f;
   if (k < K) {
 #pragma unroll 8
@@ -497,6 +530,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   __syncthreads();
   if (ty != 0 || k >= K) return;
   for (int r = 1; r < FIN_ROWS; ++r) { a += sa[r][tx]; b += sb[r][tx]; }
+  }
   sums[k] = a;
   sums[K + k] = b;
   if (dgamma != nullptr) {
@@ -505,7 +539,7 @@ __global__ void __launch_bounds__(256) bn_bwd_part_kernel(const float* __restric
   }
 }
 
-size_t bn_bwd_part_ws_floats(int G, int K) { return (size_t)ceil_div(G, FIN_GPB) * 2 * K; }
+size_t bn_bwd_part_ws_floats(int G, int K) { return (size_t)ceil_div(G, fin_gpb(G)) * 2 * K; }
 
 void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                               const float* stats, int mask, int64_t M, int K, float* ws,
@@ -652,16 +686,17 @@ void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uin
 
 void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float* sums,
                                const float* invstd, float* dgamma, float* dbeta, hipStream_t st) {
-  const int P = ceil_div(G, FIN_GPB);
+  const int gpb = fin_gpb(G);
+  const int P = ceil_div(G, gpb);
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn reduce: too many channels");
   if (bn_lastblock()) {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 0, P, counter_bank(st));
+                       sums, invstd, dgamma, dbeta, 0, P, P > 1 ? counter_bank(st) : 0, gpb);
   } else {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 1, P, 0);
+                       sums, invstd, dgamma, dbeta, 1, P, 0, gpb);
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), 1), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 2, P, 0);
+                       sums, invstd, dgamma, dbeta, 2, P, 0, gpb);
   }
 }
 
