@@ -734,10 +734,21 @@ class _ResidualBlock(torch.autograd.Function):
         # fp8io = (x8, per-chain-unit _Q8State list, holder for the output's e4m3 copy) or None
         x8, q8s, holder = fp8io if fp8io is not None else (None, None, None)
         # shortcut first (it only needs x) so its output can be freed into the tail's add
+        ds_join = None
         if ds_cfg is not None:
             w, g, b, rm, rv = tensors[5 * nch:5 * nch + 5]
             st, pd, tr, mo, ep = ds_cfg
-            if q8s is None and _FUSE_RES_BN:
+            br = streams.branch_stream(x.device) if x.is_cuda and nch > 1 else None
+            if q8s is None and _FUSE_RES_BN and br is not None:
+                # projection shortcut on the branch stream, concurrent with the chain's first
+                # units; the tail unit (which applies its BN inside the residual add) waits
+                buffers_ready()  # a deferred BN-buffer wait lands on this stream, before the fork
+                main = streams.fork(br, x)
+                with torch.cuda.stream(br):
+                    y_ds, st_ds = _unit_conv_stats(C, x, w, g, b, rm, rv, st, pd, tr, mo, ep, x8)
+                ds_join = (main, streams.join(br, main, y_ds, st_ds))
+                res = (y_ds, st_ds)
+            elif q8s is None and _FUSE_RES_BN:
                 # projection shortcut: conv + statistics only; its BN apply runs inside the block
                 # tail's apply pass (bn_act_fwd RESBN), so the normalised shortcut is never stored
                 y_ds, st_ds = _unit_conv_stats(C, x, w, g, b, rm, rv, st, pd, tr, mo, ep, x8)
@@ -752,6 +763,8 @@ class _ResidualBlock(torch.autograd.Function):
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
             last = i == nch - 1
+            if last and ds_join is not None:
+                ds_join[0].wait_event(ds_join[1])
             # the block output's ReLU mask as bits: the next block's BN-fused dgrad reads it
             # instead of z (1/16 of the bytes)
             z, y, stt, h8, zm = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
@@ -870,6 +883,29 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j + 2] = sums_[0]
             return g_, sums_
 
+        def shortcut_backward(g_short_):
+            """projection shortcut: BN backward (reduce + apply), weight gradient, and the input
+            gradient that the first conv's dgrad epilogue adds (None when x needs none)"""
+            st2, pd2, tr2, _, _ = ds_cfg
+            wds = tensors[5 * nch]
+            sums_ds = bnreduce(5 * nch, g_short_, g_short_, y_ds, st_ds, 0)
+            dy_ds, _, d8_ds = apply(5 * nch, g_short_, g_short_, y_ds, st_ds, sums_ds, 0, tr2, False,
+                                    ctx.needs_input_grad[0])
+            wgrad(5 * nch, dy_ds, x, st2, pd2)
+            if not ctx.needs_input_grad[0]:
+                return None
+            if st2 == 2 and pd2 == 0 and wds.shape[2] == 1 and wds.shape[3] == 1 and _COMPACT_ADDEND:
+                # 1x1/s2 shortcut: its input gradient is zero at every odd (h, w), so it is
+                # computed as a dense 1x1 dgrad on the stride-2 grid and the first conv's
+                # dgrad epilogue adds it at even positions only (no full-resolution tensor,
+                # no all-zero parity-class launches)
+                n_, h_, w_, c_ = x.shape
+                return dgrad(dy_ds, d8_ds, wds, [n_, (h_ + 1) // 2, (w_ + 1) // 2, c_], 1, 0, None)
+            return dgrad(dy_ds, d8_ds, wds, list(x.shape), st2, pd2, None)
+
+        ds_br = streams.branch_stream(x.device) if ds_cfg is not None and x.is_cuda else None
+        ds_join = None
+
         # gradient arriving pre-masked and pre-reduced from the next block's dgrad epilogue?
         pre = None
         ho = ctx.handoff_out
@@ -906,6 +942,13 @@ class _ResidualBlock(torch.autograd.Function):
             wgrad(5 * i, dy, xin, st, pd)
             if last:
                 g_short = dres
+                if ds_cfg is not None and nch > 1 and ds_br is not None:
+                    # projection-shortcut backward on the branch stream, concurrent with the
+                    # chain's remaining units; the first conv's dgrad waits for its addend
+                    main = streams.fork(ds_br, g_short, y_ds, st_ds, x)
+                    with torch.cuda.stream(ds_br):
+                        addend_br = shortcut_backward(g_short)
+                    ds_join = (main, streams.join(ds_br, main, addend_br), addend_br)
             if i > 0:
                 yp, sttp = units[i - 1][1], units[i - 1][2]
                 if _FUSE_DGRAD_BN:
@@ -914,22 +957,11 @@ class _ResidualBlock(torch.autograd.Function):
                     dz = dgrad(dy, d8, w, list(xin.shape), st, pd, None)
             else:
                 # shortcut gradient: identity -> g_short itself; projection -> its dgrad
-                if ds_cfg is not None:
-                    st2, pd2, tr2, _, _ = ds_cfg
-                    wds = tensors[5 * nch]
-                    sums_ds = bnreduce(5 * nch, g_short, g_short, y_ds, st_ds, 0)
-                    dy_ds, _, d8_ds = apply(5 * nch, g_short, g_short, y_ds, st_ds, sums_ds, 0, tr2, False,
-                                            ctx.needs_input_grad[0])
-                    wgrad(5 * nch, dy_ds, x, st2, pd2)
-                    if st2 == 2 and pd2 == 0 and wds.shape[2] == 1 and wds.shape[3] == 1 and _COMPACT_ADDEND:
-                        # 1x1/s2 shortcut: its input gradient is zero at every odd (h, w), so it is
-                        # computed as a dense 1x1 dgrad on the stride-2 grid and the first conv's
-                        # dgrad epilogue adds it at even positions only (no full-resolution tensor,
-                        # no all-zero parity-class launches)
-                        n_, h_, w_, c_ = x.shape
-                        addend = dgrad(dy_ds, d8_ds, wds, [n_, (h_ + 1) // 2, (w_ + 1) // 2, c_], 1, 0, None)
-                    else:
-                        addend = dgrad(dy_ds, d8_ds, wds, list(x.shape), st2, pd2, None)
+                if ds_join is not None:
+                    ds_join[0].wait_event(ds_join[1])
+                    addend = ds_join[2]
+                elif ds_cfg is not None:
+                    addend = shortcut_backward(g_short)
                 else:
                     addend = g_short
                 if not ctx.needs_input_grad[0]:
