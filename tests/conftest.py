@@ -37,3 +37,31 @@ def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+@pytest.fixture(autouse=True)
+def _keepalive(request):
+    """GPU tests that compile library kernels on a fresh box (MIOpen for the stock-model
+    yardsticks) can run a minute without printing; a daemon thread writes a progress mark to the
+    real stderr (past pytest's capture) every 30 s so a runner's no-output watchdog sees a live
+    process."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import threading
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(30.0):
+            try:
+                sys.__stderr__.write(f"[keepalive] {request.node.name} still running\n")
+                sys.__stderr__.flush()
+            except Exception:
+                return
+
+    t = threading.Thread(target=beat, daemon=True)
+    t.start()
+    try:
+        yield
+    finally:
+        stop.set()
