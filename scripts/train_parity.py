@@ -44,6 +44,9 @@ def accuracy(model, ds, native, bs=500):
 
 
 def main():
+    # stock convolutions through PyTorch's own im2col + BLAS path, not MIOpen: on a fresh box MIOpen
+    # compiles every conv shape first (minutes, silently), and the fp32 reference needs no MIOpen
+    torch.backends.cudnn.enabled = False
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=128)

@@ -65,3 +65,18 @@ def _keepalive(request):
         yield
     finally:
         stop.set()
+
+
+@pytest.fixture(autouse=True)
+def _stock_convs_without_miopen(request):
+    """Stock-PyTorch yardstick models in GPU tests run their convolutions without MIOpen
+    (PyTorch's own im2col + BLAS path).  On a fresh box MIOpen compiles every new conv shape
+    inside the conv call while holding the GIL -- minutes for a ResNet-50 in fp32 and bf16,
+    train and eval -- so no output (not even the keepalive thread's) appears meanwhile.  The
+    yardsticks only need correct fp32 / bf16 convolutions, not MIOpen's."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+    with torch.backends.cudnn.flags(enabled=False):
+        yield
