@@ -756,24 +756,27 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
         ooff[it] = OOB;
         aoff[it] = OOB;
         if (m < P.M && col < P.Nout) {
-          int64_t orow = m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel index
+          // 32-bit offsets: every operand is addressed through a buffer resource (< 4 GiB)
+          uint32_t orow = (uint32_t)m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel
           if (!P.dense || (HA && P.add_sub)) {
             uint32_t n = fdiv((uint32_t)m, P.div_ij);
             uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
             uint32_t ii = fdiv(rem, P.div_j);
             uint32_t jj = rem - ii * (uint32_t)P.Mj;
             if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
-              orow = ((int64_t)n * P.OH + ii * P.osh + P.oph) * P.OW + jj * P.osw + P.opw;
+              orow = (n * (uint32_t)P.OH + ii * (uint32_t)P.osh + (uint32_t)P.oph) * (uint32_t)P.OW +
+                     jj * (uint32_t)P.osw + (uint32_t)P.opw;
             if (HA && P.add_sub) {
               // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
               // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
               const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
               const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
               if (((hh | ww) & 1) == 0)
-                aoff[it] = (uint32_t)(((((int64_t)n * P.add_h + (hh >> 1)) * P.add_w + (ww >> 1)) * P.Nout + col) * 2);
+                aoff[it] = (((n * (uint32_t)P.add_h + (uint32_t)(hh >> 1)) * (uint32_t)P.add_w + (uint32_t)(ww >> 1)) *
+                                (uint32_t)P.Nout + (uint32_t)col) * 2u;
             }
           }
-          ooff[it] = (uint32_t)((orow * P.Nout + col) * 2);
+          ooff[it] = (orow * (uint32_t)P.Nout + (uint32_t)col) * 2u;
           if (HA && !P.add_sub) aoff[it] = ooff[it];
         }
       }
@@ -829,7 +832,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
             const float g = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
             a.v[q] = g;
             bsg[q] += g;
-            bsq[q] = fmaf(g, yy.v[q] - bmu[q], bsq[q]);
+            bsq[q] = fmaf(g, yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
           }
           v = __builtin_bit_cast(v4i, pack8(a));
         }
@@ -855,6 +858,10 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
     if (has_add) run_batches(M0{}, HT{}); else run_batches(M0{}, HF{});
   }
   if constexpr (EPI == EPI_BNB) {
+    // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
+    // loop above (the epilogue, not the MFMAs, bounds the short-K dgrads' issue)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bsq[q] = fmaf(-bmu[q], bsg[q], bsq[q]);
     // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
     // first CH_PER_ROW lanes write this wave's (rows group, channels) partials
 #pragma unroll
