@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import warnings
 from typing import List, Optional
 
 import torch
@@ -197,7 +198,19 @@ class DistributedDataParallel(nn.Module):
             raise RuntimeError("comm='rccl' needs a CUDA device, the nccl backend (or force_reducer "
                                "in a single process) and the native extension")
         if self._collective and use_native:
-            self.comm = pcomm.native_comm(self.device, process_group)
+            try:
+                self.comm = pcomm.native_comm(self.device, process_group)
+            except RuntimeError as e:
+                if comm == "rccl":
+                    raise
+                warnings.warn(f"native RCCL communicator unavailable ({e}); gradients are reduced "
+                              "through torch.distributed collectives instead")
+            if self.world_size > 1 and comm != "rccl":
+                # every rank must take the same path: native on all or on none
+                ok = torch.tensor([0 if self.comm is None else 1], dtype=torch.int32, device=self.device)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=process_group)
+                if int(ok.item()) == 0:
+                    self.comm = None
         # the buffer-broadcast wait can move to the first BatchNorm only where every buffer
         # reader is one of our BN kernels (ops.buffers_ready): the native device model
         self._defer_buffer_wait = (self.comm is not None and getattr(module, "impl", None) == "native"
