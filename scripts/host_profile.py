@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Where the host's issue time goes: cProfile over eager training steps of the native model.
+
+    python scripts/host_profile.py [arch] [image] [batch] [steps]   (default resnet18 32 256 50)
+
+Prints the synchronized ms/step, the host ms/step, and the top functions by own time and by
+cumulative time.  The CIFAR-shaped ResNet-18 step is host-bound, so every microsecond of Python
+per step shows up in its eager throughput.
+"""
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_tutorials_amd import ops  # noqa: E402
+from pytorch_distributed_tutorials_amd.models import build_model  # noqa: E402
+from pytorch_distributed_tutorials_amd.optim import SGD  # noqa: E402
+from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel  # noqa: E402
+
+
+def main():
+    arch = sys.argv[1] if len(sys.argv) > 1 else "resnet18"
+    image = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 50
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = build_model(arch, num_classes=10 if image <= 64 else 1000, impl="native").to(dev)
+    model.set_impl("native")
+    ddp = DistributedDataParallel(model)
+    opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+    crit = ops.CrossEntropyLoss()
+    x = torch.randn(batch, 3, image, image, device=dev)
+    y = torch.randint(0, 10, (batch,), device=dev)
+
+    def step():
+        opt.zero_grad()
+        loss = crit(ddp(x), y)
+        loss.backward()
+        opt.step()
+
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    sync_ms = (time.perf_counter() - t0) * 1e3 / steps
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    for _ in range(steps):
+        step()
+    pr.disable()
+    host_ms = (time.perf_counter() - t0) * 1e3 / steps
+    torch.cuda.synchronize()
+    print(f"{arch} {image}px batch {batch}: {sync_ms:.3f} ms/step synchronized, {host_ms:.3f} ms/step host "
+          f"under cProfile", flush=True)
+    for key in ("tottime", "cumulative"):
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(35)
+        print(s.getvalue(), flush=True)
+
+
+if __name__ == "__main__":
+    main()
