@@ -7,6 +7,7 @@
 // communicator and the gradient reducer.
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -15,6 +16,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 
 #include "comm/rccl_comm.h"
 #include "ddp/reducer.h"
@@ -366,6 +368,35 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
                          s, deterministic, false, cur_stream(x));
   Tensor krsc = Cx == C ? dwp : dwp.narrow(3, 0, C).contiguous();
   return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
+}
+
+// conv_wgrad issued on the weight-gradient side stream (ops/fused.py, ops/streams.py) in one call:
+// the side stream waits for the work queued so far on the current stream (one reusable event per
+// device: a wait binds to the record made just before it), the wgrad runs with the side stream as
+// the current stream (its workspace is allocated for that stream), and dy / x are recorded for the
+// side stream so the caching allocator keeps their memory until it is done.  Replaces torch's
+// wait_stream + stream context + two record_stream calls: ~25 us of host issue per weight
+// gradient (scripts/host_profile.py), 20-53 of them per step.
+Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vector<int64_t> ws,
+                       int64_t stride, int64_t pad, bool deterministic, const std::optional<Tensor>& out) {
+  TORCH_CHECK(side != 0, "conv_wgrad_side: null side stream");
+  c10::hip::HIPGuard g(x.get_device());
+  const auto dev = (c10::DeviceIndex)x.get_device();
+  static thread_local std::unordered_map<int, hipEvent_t> evs;
+  hipEvent_t& ev = evs[(int)dev];
+  if (ev == nullptr)
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+  auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
+  TORCH_CHECK(hipEventRecord(ev, c10::hip::getCurrentHIPStream(dev).stream()) == hipSuccess, "hipEventRecord failed");
+  TORCH_CHECK(hipStreamWaitEvent(sst.stream(), ev, 0) == hipSuccess, "hipStreamWaitEvent failed");
+  Tensor r;
+  {
+    c10::hip::HIPStreamGuard sg(sst);
+    r = conv_wgrad(dy, x, ws, stride, pad, deterministic, out);
+  }
+  c10::hip::HIPCachingAllocator::recordStream(dy.storage().data_ptr(), sst);
+  c10::hip::HIPCachingAllocator::recordStream(x.storage().data_ptr(), sst);
+  return r;
 }
 
 // -------------------------------------------------------------------- stem
@@ -1076,6 +1107,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta") = py::none(), py::arg("wt") = py::none());
   m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
+  m.def("conv_wgrad_side", checked("conv_wgrad_side", &conv_wgrad_side), py::arg("side"), py::arg("dy"),
+        py::arg("x"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("deterministic") = false,
+        py::arg("out") = py::none());
   m.def("stem_conv_fwd", checked("stem_conv_fwd", &stem_conv_fwd), py::arg("x"), py::arg("w"),
         py::arg("stride"), py::arg("pad"), py::arg("stats"));
   m.def("stem_wgrad", checked("stem_wgrad", &stem_wgrad), py::arg("dy"), py::arg("xsp"),

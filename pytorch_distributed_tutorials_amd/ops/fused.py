@@ -596,9 +596,21 @@ class bump_bn_counters:
     issued by the first BN of the forward (``buffers_ready``), behind any buffer broadcast."""
 
     def __init__(self, module: nn.Module):
-        self.counters = [m.num_batches_tracked for m in module.modules()
-                         if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.training
-                         and m.track_running_stats and m.num_batches_tracked is not None]
+        # the counter list is cached on the module: walking every submodule each forward cost
+        # ~80 us of host issue per ResNet-18 step (scripts/host_profile.py).  Keyed by what
+        # selects the counters (each BN's mode and buffer), so train()/eval() or a replaced
+        # buffer rebuilds it.
+        bns = getattr(module, "_pdt_bn_list", None)
+        if bns is None:
+            bns = [m for m in module.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+            module._pdt_bn_list = bns
+        key = tuple((m.training, m.track_running_stats, id(m.num_batches_tracked)) for m in bns)
+        cached = getattr(module, "_pdt_bn_counters", None)
+        if cached is None or cached[0] != key:
+            cached = (key, [m.num_batches_tracked for m in bns if m.training and m.track_running_stats
+                            and m.num_batches_tracked is not None])
+            module._pdt_bn_counters = cached
+        self.counters = cached[1]
 
     def __enter__(self):
         global _NBT_BATCHED, _PENDING_BUMP
@@ -824,9 +836,8 @@ class _ResidualBlock(torch.autograd.Function):
             if sink is not None:
                 # weight gradient into the flat buffer on the side stream, concurrent with the
                 # dgrad chain; all-reduce and optimizer wait for that stream (streams.py)
-                if side is not None:
-                    streams.launch(side, lambda: C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_,
-                                                              det, sink), dy_, xin_)
+                if side is not None:  # one native call: stream hand-off, launch, record_stream
+                    C.conv_wgrad_side(side.cuda_stream, dy_, xin_, list(w_.shape), st_, pd_, det, sink)
                 else:
                     C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det, sink)
                 sunk.append(params[j])

@@ -54,10 +54,13 @@ def main():
     sync_ms = (time.perf_counter() - t0) * 1e3 / steps
     pr = cProfile.Profile()
     t0 = time.perf_counter()
-    pr.enable()
-    for _ in range(steps):
-        step()
-    pr.disable()
+    # backward on this thread (not the autograd engine's device thread), so cProfile sees the
+    # Python backward functions too
+    with torch.autograd.set_multithreading_enabled(False):
+        pr.enable()
+        for _ in range(steps):
+            step()
+        pr.disable()
     host_ms = (time.perf_counter() - t0) * 1e3 / steps
     torch.cuda.synchronize()
     print(f"{arch} {image}px batch {batch}: {sync_ms:.3f} ms/step synchronized, {host_ms:.3f} ms/step host "
