@@ -240,9 +240,14 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
   }
   const int G = pdt::conv_dgrad_bn_groups(s, (int)dy_like.element_size());
   auto fopt = y.options().dtype(at::kFloat);
-  auto part = at::empty({(int64_t)G * 2 * s.C}, fopt);
-  auto ws = at::empty({(int64_t)pdt::bn_bwd_part_ws_floats(G, s.C)}, fopt);
-  auto sums = at::empty({2, s.C}, fopt);
+  // sums, partials and the reduction workspace as slices of ONE allocation (host issue: each
+  // caching-allocator call is ~1-2 us, and this binding runs once per BatchNorm per step)
+  const int64_t n_sums = 2 * (int64_t)s.C, n_part = (int64_t)G * 2 * s.C;
+  const int64_t n_ws = (int64_t)pdt::bn_bwd_part_ws_floats(G, s.C);
+  auto fbuf = at::empty({n_sums + n_part + n_ws}, fopt);
+  auto sums = fbuf.narrow(0, 0, n_sums).view({2, s.C});
+  auto part = fbuf.narrow(0, n_sums, n_part);
+  auto ws = fbuf.narrow(0, n_sums + n_part, n_ws);
   pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
   hipStream_t st = cur_stream(dy_like);
   launch(s, bf(dx), ap, &bn, st, asub);
