@@ -66,8 +66,10 @@ class BasicBlock(nn.Module):
 
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:  # one fused autograd node per block on the device path
-            ds = (self.downsample[0], self.downsample[1]) if self.downsample is not None else None
-            return ops.residual_block(x, [(self.conv1, self.bn1), (self.conv2, self.bn2)], ds)
+            m = self._modules  # direct dict reads: nn.Module.__getattr__ is a slow fallback path
+            d = m.get("downsample")  # None is a plain attribute, not in _modules
+            ds = (d[0], d[1]) if d is not None else None
+            return ops.residual_block(x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"])], ds)
         out = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
         identity = x
         if self.downsample is not None:
@@ -103,9 +105,11 @@ class Bottleneck(nn.Module):
 
     def forward_native(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:  # one fused autograd node per block on the device path
-            ds = (self.downsample[0], self.downsample[1]) if self.downsample is not None else None
+            m = self._modules  # direct dict reads: nn.Module.__getattr__ is a slow fallback path
+            d = m.get("downsample")  # None is a plain attribute, not in _modules
+            ds = (d[0], d[1]) if d is not None else None
             return ops.residual_block(
-                x, [(self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)], ds)
+                x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"]), (m["conv3"], m["bn3"])], ds)
         identity = x
         if self.downsample is not None:
             identity = ops.conv_bn(x, self.downsample[0], self.downsample[1], relu=False)
@@ -161,6 +165,7 @@ class ResNet(nn.Module):
         if impl not in ("torch", "native"):
             raise ValueError(f"unknown impl {impl!r}")
         self.impl = impl
+        ops.forget_bn_modules(self)  # re-collected at the next device forward
         if impl == "native":
             for m in self.modules():
                 if isinstance(m, nn.Conv2d):

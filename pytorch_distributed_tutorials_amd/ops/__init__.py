@@ -11,6 +11,7 @@ from .fused import (  # noqa: F401
     avgpool_linear,
     buffers_ready,
     bump_bn_counters,
+    forget_bn_modules,
     defer_buffer_wait,
     conv_bn,
     cross_entropy,

@@ -588,6 +588,13 @@ def _counter_flat(counters):
     return base
 
 
+def forget_bn_modules(module: nn.Module) -> None:
+    """Drop the BatchNorm list ``bump_bn_counters`` caches on ``module`` (collected at its first
+    device forward).  Call after replacing or adding BatchNorm submodules; ``set_impl`` does."""
+    module.__dict__.pop("_pdt_bn_list", None)
+    module.__dict__.pop("_pdt_bn_counters", None)
+
+
 class bump_bn_counters:
     """Context for one device forward of a whole model: bumps every training BatchNorm's
     ``num_batches_tracked`` (torch BN semantics) with ONE multi-tensor launch
@@ -1003,6 +1010,14 @@ def _grad_sink(p):
     return sp.grad_sink(p)
 
 
+def _unit_tensors(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> list:
+    """(weight, gamma, beta, running_mean, running_var) of one conv+BN unit, read from the module
+    dicts directly: nn.Module.__getattr__'s fallback path for parameters and buffers was ~40 us of
+    host issue per ResNet-18 step (scripts/host_profile.py)."""
+    bp, bb = bn._parameters, bn._buffers
+    return [conv._parameters["weight"], bp["weight"], bp["bias"], bb["running_mean"], bb["running_var"]]
+
+
 def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
     """Device path of a ResNet block: ``chain`` = [(conv, bn), ...] (ReLU after each BN, the
     shortcut added before the last ReLU), ``downsample`` = (conv, bn) or None."""
@@ -1010,13 +1025,13 @@ def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
     for conv, bn in chain:
         tr, mo, ep = _bn_prepare(bn)
         spec_chain.append((conv.stride[0], conv.padding[0], tr, mo, ep))
-        tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+        tensors += _unit_tensors(conv, bn)
     ds_spec = None
     if downsample is not None:
         conv, bn = downsample
         tr, mo, ep = _bn_prepare(bn)
         ds_spec = (conv.stride[0], conv.padding[0], tr, mo, ep)
-        tensors += [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+        tensors += _unit_tensors(conv, bn)
     fp8io = None
     if _FP8:
         q8s = [_q8_state(bn, x.device) for _, bn in chain]

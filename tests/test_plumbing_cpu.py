@@ -245,3 +245,24 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
     assert d["config"]["global_batch"] == 8 and d["config"]["parallelism"] == "dp2"
     assert abs(d["value"] - 8 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
+
+
+def test_bn_counter_list_cache_follows_mode_and_surgery():
+    """bump_bn_counters caches the model's BatchNorm list (host issue); the cached counters follow
+    train()/eval() and a replaced counter buffer, and forget_bn_modules picks up new modules."""
+    import torch.nn as nn
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    m = build_model("resnet18", num_classes=10)
+    nbn = sum(isinstance(x, nn.BatchNorm2d) for x in m.modules())
+    assert len(ops.bump_bn_counters(m).counters) == nbn
+    m.eval()
+    assert ops.bump_bn_counters(m).counters == []
+    m.train()
+    c = ops.bump_bn_counters(m).counters
+    assert len(c) == nbn and c[0] is m.bn1.num_batches_tracked
+    m.bn1.num_batches_tracked = torch.zeros((), dtype=torch.long)  # re-homed buffer
+    assert ops.bump_bn_counters(m).counters[0] is m.bn1.num_batches_tracked
+    m.bn1 = nn.BatchNorm2d(64)  # module surgery: invisible until forgotten
+    ops.forget_bn_modules(m)
+    assert ops.bump_bn_counters(m).counters[0] is m.bn1.num_batches_tracked
