@@ -266,3 +266,30 @@ def test_bn_counter_list_cache_follows_mode_and_surgery():
     m.bn1 = nn.BatchNorm2d(64)  # module surgery: invisible until forgotten
     ops.forget_bn_modules(m)
     assert ops.bump_bn_counters(m).counters[0] is m.bn1.num_batches_tracked
+
+
+def test_sgd_flat_space_check_cache_tracks_the_param_list():
+    """optim.SGD caches 'this group is exactly one flat space' per group (host issue); a changed
+    member invalidates it, and nothing of the cache leaks into state_dict()."""
+    from pytorch_distributed_tutorials_amd.optim import SGD
+
+    class _Space:
+        pass
+
+    ps = [nn.Parameter(torch.zeros(2)) for _ in range(3)]
+    sp = _Space()
+    sp.params = list(ps)
+    for p in ps:
+        p._pdt_flat = sp
+    opt = SGD(ps, lr=0.1, momentum=0.9)
+    g = opt.param_groups[0]
+    assert opt._flat_space_of(g) is sp
+    assert opt._flat_space_of(g) is sp  # cached path
+    other = nn.Parameter(torch.zeros(2))
+    other._pdt_flat = sp
+    g["params"][2] = other  # same length, different member: not the space any more
+    assert opt._flat_space_of(g) is None
+    g["params"][2] = ps[2]
+    assert opt._flat_space_of(g) is sp
+    assert set(opt.state_dict()["param_groups"][0]) == set(g) - {"params"} | {"params"}
+    assert not any(k.startswith("_pdt") for k in opt.state_dict()["param_groups"][0])
