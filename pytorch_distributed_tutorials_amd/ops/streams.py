@@ -8,7 +8,8 @@ stays on the caller's stream (it is the critical path of backward).
 
 Ordering: the side stream waits for the caller's stream before each wgrad (its
 inputs are ready); the inputs are ``record_stream``-ed so the caching allocator
-does not hand their memory out while the side stream still reads them; gradient
+does not hand their memory out while the side stream still reads them -- all three
+in one native call, ``C.conv_wgrad_side`` (csrc/bindings.cpp); gradient
 all-reduces wait for the side stream (``Reducer.set_aux_stream``); and a callback
 at the end of backward joins it into the caller's stream, so the optimizer step
 sees every gradient.  ``PDT_WGRAD_STREAM=0`` turns it off.
@@ -104,15 +105,3 @@ def begin(device: torch.device) -> Optional[torch.cuda.Stream]:
         cur = torch.cuda.current_stream(device)
         torch.autograd.Variable._execution_engine.queue_callback(lambda: cur.wait_stream(s))
     return s
-
-
-def launch(side: torch.cuda.Stream, fn, *inputs: torch.Tensor):
-    """Run ``fn()`` on the side stream after the caller's stream reached this point; keeps the
-    (caller-stream-allocated) ``inputs`` alive for the side stream's reads."""
-    side.wait_stream(torch.cuda.current_stream(side.device))
-    with torch.cuda.stream(side):
-        out = fn()
-    for t in inputs:
-        t.record_stream(side)
-    return out
-
