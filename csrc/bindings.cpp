@@ -387,6 +387,8 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
   TORCH_CHECK(side != 0, "conv_wgrad_side: null side stream");
   c10::hip::HIPGuard g(x.get_device());
   const auto dev = (c10::DeviceIndex)x.get_device();
+  // per calling thread (autograd runs a device's backward on one long-lived engine thread) and
+  // device; kept for the process lifetime like torch's own stream pool
   static thread_local std::unordered_map<int, hipEvent_t> evs;
   hipEvent_t& ev = evs[(int)dev];
   if (ev == nullptr)
