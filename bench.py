@@ -72,6 +72,14 @@ def parse(argv=None):
                    help="capture the whole training step in a HIP graph and replay it (native impl)")
     p.add_argument("--fp8", action="store_true",
                    help="native impl: forward convs on the fp8 (e4m3) MX-rate MFMA, delayed scaling")
+    p.add_argument("--watchdog-timeout", type=float, default=None,
+                   help="abort a rank that makes no progress for N seconds (default 600 when N > 1, "
+                        "off for one process; 0 = off): a dead peer ends the run instead of hanging it")
+    p.add_argument("--comm-timeout", type=float, default=None,
+                   help="native RCCL communicator: init / per-collective timeout in seconds (600)")
+    p.add_argument("--rccl-channels", default=None,
+                   help="native RCCL communicator channel bounds 'min[,max]' (ncclConfig_t "
+                        "minCTAs/maxCTAs; default: RCCL's choice)")
     p.add_argument("--cudnn-benchmark", action="store_true",
                    help="stock path: let MIOpen search for the fastest conv solutions")
     return p.parse_args(argv)
@@ -117,18 +125,33 @@ def main(argv=None) -> int:
         from pytorch_distributed_tutorials_amd.utils.seed import set_random_seeds
         set_random_seeds(0, deterministic=True)
 
+    from pytorch_distributed_tutorials_amd.utils.watchdog import Watchdog
+    wd_timeout = args.watchdog_timeout if args.watchdog_timeout is not None else (600.0 if world > 1 else 0.0)
+    holder = {}
+    watchdog = None
+    if wd_timeout > 0:
+        watchdog = Watchdog(wd_timeout, rank=env.rank,
+                            on_timeout=lambda: holder["ddp"].abort() if "ddp" in holder else None)
+        watchdog.heartbeat("setup")
+
     if args.fp8:
         if args.impl != "native":
             raise SystemExit("--fp8 needs --impl native")
         ops.set_fp8(True)
     if args.impl == "native":
+        from pytorch_distributed_tutorials_amd.parallel.comm import CommOptions
+        copts = CommOptions.from_env(timeout=args.comm_timeout)
+        if args.rccl_channels:
+            ch = [int(v) for v in args.rccl_channels.split(",")]
+            copts.min_channels, copts.max_channels = ch[0], ch[-1]
         model = build_model(args.arch, num_classes=args.num_classes, impl="native").to(dev)
         model.set_impl("native")
         ddp = DistributedDataParallel(model, device_ids=dev_ids, output_device=dev_ids and dev_index,
                                       bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                                       first_bucket_mb=args.first_bucket_mb,
                                       last_bucket_mb=args.last_bucket_mb,
-                                      force_reducer=args.force_comm)
+                                      force_reducer=args.force_comm, comm_options=copts)
+        holder["ddp"] = ddp
         if args.comm_timing:
             ddp.enable_comm_timing(True)
         opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
@@ -181,12 +204,19 @@ def main(argv=None) -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    def beat(phase):
+        if watchdog is not None:
+            watchdog.heartbeat(phase)
+
+    for i in range(args.warmup):
+        beat(f"warmup {i}")
         loss = step()
+    beat("barrier")
     barrier()
     t0 = time.perf_counter()
     host = 0.0  # host time spent inside step() (issue time; ~= step time when the host is the bound)
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        beat(f"step {i}")
         th = time.perf_counter()
         loss = step()
         host += time.perf_counter() - th
@@ -240,6 +270,8 @@ def main(argv=None) -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if watchdog is not None:
+        watchdog.stop()
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -1199,15 +1199,28 @@ PYBIND11_MODULE(_C, m) {
     d["bm"] = out[0]; d["bn"] = out[1]; d["tiles"] = out[2]; d["splits"] = out[3];
     return d;
   }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("deterministic") = false);
+  m.def("bn_counter_bank", [](uintptr_t stream) {
+    return pdt::bn_counter_bank(reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("stream"));
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });
 
   py::class_<pdt::RcclComm, std::shared_ptr<pdt::RcclComm>>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(pdt::RcclComm::unique_id()); })
-      .def(py::init([](const std::string& uid, int rank, int world, int device) {
-             py::gil_scoped_release nogil;  // ncclCommInitRank blocks until all ranks join
-             return std::make_shared<pdt::RcclComm>(uid, rank, world, device);
-           }))
+      .def(py::init([](const std::string& uid, int rank, int world, int device, double init_timeout,
+                       double op_timeout, bool exit_on_error, int min_channels, int max_channels) {
+             py::gil_scoped_release nogil;  // init polls until every rank joined (or the deadline)
+             pdt::RcclOptions o;
+             o.init_timeout_s = init_timeout;
+             o.op_timeout_s = op_timeout;
+             o.exit_on_error = exit_on_error;
+             o.min_channels = min_channels;
+             o.max_channels = max_channels;
+             return std::make_shared<pdt::RcclComm>(uid, rank, world, device, o);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("init_timeout") = 600.0, py::arg("op_timeout") = 600.0,
+           py::arg("exit_on_error") = false, py::arg("min_channels") = 0, py::arg("max_channels") = 0)
       .def_property_readonly("rank", &pdt::RcclComm::rank)
       .def_property_readonly("world", &pdt::RcclComm::world)
       .def_property_readonly("device", &pdt::RcclComm::device)
@@ -1225,7 +1238,12 @@ PYBIND11_MODULE(_C, m) {
       .def("current_wait_comm", &pdt::RcclComm::current_wait_comm)
       .def("synchronize", &pdt::RcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &pdt::RcclComm::barrier, py::call_guard<py::gil_scoped_release>())
-      .def("abort", &pdt::RcclComm::abort);
+      .def("abort", &pdt::RcclComm::abort)
+      .def("check", &pdt::RcclComm::check)
+      .def_property_readonly("healthy", &pdt::RcclComm::healthy)
+      .def_property_readonly("error", &pdt::RcclComm::error)
+      .def_property_readonly("init_seconds", &pdt::RcclComm::init_seconds)
+      .def("inject_delay", &pdt::RcclComm::inject_delay, py::arg("seconds"));
 
   py::class_<pdt::Reducer>(m, "Reducer")
       .def(py::init<std::vector<Tensor>, std::vector<Tensor>, std::vector<int64_t>, std::vector<Tensor>,

@@ -2,10 +2,16 @@
 
 #include <c10/hip/HIPGuard.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 namespace pdt {
+
+// Exit status of a process ended by the communicator monitor: the watchdog's (utils/watchdog.py
+// EXIT_CODE), so the launcher reports both the same way.
+constexpr int kCommExitCode = 124;
 
 void rccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) {
@@ -15,6 +21,10 @@ void rccl_check(ncclResult_t r, const char* what) {
 
 static void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static double since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 std::string RcclComm::unique_id() {
@@ -33,33 +43,204 @@ static bool comm_high_priority() {
   return e && e[0] == '1';
 }
 
-RcclComm::RcclComm(const std::string& uid, int rank, int world, int device)
-    : rank_(rank), world_(world), device_(device),
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, const RcclOptions& opt)
+    : rank_(rank), world_(world), device_(device), opt_(opt),
       stream_(c10::hip::getStreamFromPool(comm_high_priority(), (c10::DeviceIndex)device)) {
   if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("bad RCCL unique id size");
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   ncclUniqueId id;
   memcpy(id.internal, uid.data(), sizeof(id.internal));
-  rccl_check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  // Non-blocking init polled against a deadline (ProcessGroupNCCL's init timeout): a blocking
+  // ncclCommInitRank whose peer never arrives would hang this rank forever.
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  if (opt_.min_channels > 0) cfg.minCTAs = opt_.min_channels;
+  if (opt_.max_channels > 0) cfg.maxCTAs = opt_.max_channels;
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    rccl_check(r, "ncclCommInitRankConfig");
+  }
+  ncclResult_t st = ncclInProgress;
+  while (true) {
+    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+    if (st != ncclInProgress) break;
+    if (since(t0) > opt_.init_timeout_s) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
+  init_s_ = since(t0);
+  if (st != ncclSuccess) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+    char buf[512];
+    if (st == ncclInProgress)
+      snprintf(buf, sizeof(buf),
+               "RCCL communicator init timed out after %.1f s on rank %d of %d (device %d): a peer "
+               "rank never joined (crashed, hung, or took another code path before its init)",
+               init_s_, rank, world, device);
+    else
+      snprintf(buf, sizeof(buf), "RCCL communicator init failed on rank %d of %d (device %d): %s",
+               rank, world, device, ncclGetErrorString(st));
+    throw std::runtime_error(buf);
+  }
   hip_check(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming), "hipEventCreate");
   barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
+  monitor_ = std::thread([this]() { monitor_loop(); });
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) {
-    ncclCommDestroy(comm_);
-    comm_ = nullptr;
-  }
+  stop_.store(true);
+  if (monitor_.joinable()) monitor_.join();
+  if (comm_ && !aborted_.load()) {
+    // non-blocking communicator: finalize (flushes outstanding work) must complete before
+    // destroy; a peer that died mid-teardown must not hang our exit, so the wait is bounded
+    ncclResult_t r = ncclCommFinalize(comm_);
+    ncclResult_t st = r;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclSuccess || r == ncclInProgress) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess || st != ncclInProgress) break;
+      if (since(t0) > 10.0) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (st == ncclSuccess) ncclCommDestroy(comm_);
+    else ncclCommAbort(comm_);
+  }  // aborted: ncclCommAbort already released the communicator
+  comm_ = nullptr;
   if (ev_a_) hipEventDestroy(ev_a_);
   if (ev_b_) hipEventDestroy(ev_b_);
+  for (auto& p : pending_) hipEventDestroy(p.ev);
+  for (hipEvent_t e : free_events_) hipEventDestroy(e);
 }
 
 void RcclComm::abort() {
-  if (comm_) {
-    ncclCommAbort(comm_);
-    comm_ = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (error_.empty()) error_ = "RCCL communicator was aborted";
+    failed_.store(true);  // before the abort: no new call may reach the freed communicator
   }
+  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+}
+
+void RcclComm::fail(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (failed_.load()) return;
+    error_ = msg;
+    failed_.store(true);
+  }
+  fprintf(stderr, "[rccl] rank %d: %s; aborting the communicator%s\n", rank_, msg.c_str(),
+          opt_.exit_on_error ? " and exiting" : "");
+  fflush(stderr);
+  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+  if (opt_.exit_on_error) std::_Exit(kCommExitCode);
+}
+
+void RcclComm::check() const {
+  if (failed_.load()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    throw std::runtime_error("RCCL communicator (rank " + std::to_string(rank_) + ") is unusable: " + error_);
+  }
+}
+
+std::string RcclComm::error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return error_;
+}
+
+void RcclComm::monitor_loop() {
+  const auto period = std::chrono::microseconds((int64_t)(opt_.poll_s * 1e6));
+  while (!stop_.load()) {
+    std::this_thread::sleep_for(period);
+    if (failed_.load()) continue;
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+      fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(st));
+      continue;
+    }
+    std::string timeout_msg;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (!pending_.empty()) {
+        Pending& p = pending_.front();
+        const hipError_t q = hipEventQuery(p.ev);
+        if (q == hipSuccess) {
+          free_events_.push_back(p.ev);
+          pending_.pop_front();
+          continue;
+        }
+        if (q != hipErrorNotReady) {
+          timeout_msg = std::string("completion query of '") + p.what + "' failed: " + hipGetErrorString(q);
+        } else if (opt_.op_timeout_s > 0 && since(p.t) > opt_.op_timeout_s) {
+          char buf[256];
+          snprintf(buf, sizeof(buf), "collective '%s' did not complete within %.1f s (timeout %.1f s): a "
+                   "peer rank is hung, dead or issued a different collective", p.what, since(p.t),
+                   opt_.op_timeout_s);
+          timeout_msg = buf;
+        }
+        break;
+      }
+    }
+    if (!timeout_msg.empty()) fail(timeout_msg);
+  }
+}
+
+void RcclComm::track(const char* what) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+    return;  // captured collectives run at replay; the process watchdog covers graph mode
+  std::lock_guard<std::mutex> lk(mu_);
+  hipEvent_t ev;
+  if (!free_events_.empty()) {
+    ev = free_events_.back();
+    free_events_.pop_back();
+  } else {
+    hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  }
+  hip_check(hipEventRecord(ev, stream()), "hipEventRecord");
+  pending_.push_back({ev, std::chrono::steady_clock::now(), what});
+}
+
+void RcclComm::finish(ncclResult_t r, const char* what) {
+  if (r == ncclInProgress) {  // non-blocking communicator: the call completes asynchronously
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t st = ncclInProgress;
+    while (st == ncclInProgress) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      if (st == ncclInProgress && since(t0) > opt_.init_timeout_s) break;
+      if (st == ncclInProgress) std::this_thread::yield();
+    }
+    r = st;
+    if (r == ncclInProgress) {
+      fail(std::string(what) + " still in progress after the init timeout");
+      check();
+    }
+  }
+  if (r != ncclSuccess) {
+    fail(std::string(what) + " failed: " + ncclGetErrorString(r));
+    check();
+  }
+  track(what);
+}
+
+void RcclComm::inject_delay(double seconds) {
+  check();
+  // host callback on the comm stream that sleeps: the stream (and anything tracked behind it)
+  // stalls for `seconds` exactly like a collective waiting on a slow peer, with no GPU kernel
+  // spinning and no RCCL kernel queued behind it
+  auto* secs = new double(seconds);
+  hip_check(hipLaunchHostFunc(
+                stream(),
+                [](void* p) {
+                  double* s = static_cast<double*>(p);
+                  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(*s * 1e6)));
+                  delete s;
+                },
+                secs),
+            "hipLaunchHostFunc");
+  track("inject_delay");
 }
 
 ncclDataType_t RcclComm::dtype_of(const at::Tensor& t) {
@@ -97,7 +278,11 @@ void RcclComm::current_wait_comm() {
   hip_check(hipStreamWaitEvent(cur, ev_b_, 0), "hipStreamWaitEvent");
 }
 
-void RcclComm::synchronize() { hip_check(hipStreamSynchronize(stream()), "hipStreamSynchronize"); }
+void RcclComm::synchronize() {
+  check();
+  hip_check(hipStreamSynchronize(stream()), "hipStreamSynchronize");
+  check();  // an abort while we waited: the stream drained because the collectives were killed
+}
 
 static void check_dev(const at::Tensor& t, int device) {
   if (!t.is_cuda() || t.get_device() != device || !t.is_contiguous())
@@ -105,7 +290,8 @@ static void check_dev(const at::Tensor& t, int device) {
 }
 
 void RcclComm::all_reduce_raw(void* ptr, size_t count, ncclDataType_t dt, ncclRedOp_t op) {
-  rccl_check(ncclAllReduce(ptr, ptr, count, dt, op, comm_, stream()), "ncclAllReduce");
+  check();
+  finish(ncclAllReduce(ptr, ptr, count, dt, op, comm_, stream()), "ncclAllReduce");
 }
 
 void RcclComm::all_reduce(const at::Tensor& t, const std::string& op, bool wait_current) {
@@ -116,31 +302,32 @@ void RcclComm::all_reduce(const at::Tensor& t, const std::string& op, bool wait_
 
 void RcclComm::broadcast(const at::Tensor& t, int root, bool wait_current) {
   check_dev(t, device_);
+  check();
   if (wait_current) comm_wait_current();
-  rccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), root, comm_,
-                           stream()),
-             "ncclBroadcast");
+  finish(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), root, comm_, stream()),
+         "ncclBroadcast");
 }
 
 void RcclComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, const std::string& op,
                               bool wait_current) {
   check_dev(in, device_);
   check_dev(out, device_);
+  check();
   if (in.numel() != out.numel() * world_) throw std::runtime_error("reduce_scatter: size mismatch");
   if (wait_current) comm_wait_current();
-  rccl_check(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), dtype_of(in),
-                               op_of(op), comm_, stream()),
-             "ncclReduceScatter");
+  finish(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), dtype_of(in), op_of(op),
+                           comm_, stream()),
+         "ncclReduceScatter");
 }
 
 void RcclComm::all_gather(const at::Tensor& in, const at::Tensor& out, bool wait_current) {
   check_dev(in, device_);
   check_dev(out, device_);
+  check();
   if (out.numel() != in.numel() * world_) throw std::runtime_error("all_gather: size mismatch");
   if (wait_current) comm_wait_current();
-  rccl_check(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), dtype_of(in), comm_,
-                           stream()),
-             "ncclAllGather");
+  finish(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), dtype_of(in), comm_, stream()),
+         "ncclAllGather");
 }
 
 void RcclComm::barrier() {

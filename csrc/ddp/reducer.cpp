@@ -72,6 +72,7 @@ struct ReducerState {
     const bool first = launch_order.empty();
     launch_order.push_back(b);
     if (comm) {
+      comm->check();  // a timed-out / failed communicator: raise here, out of backward()
       const at::Tensor& f = flats[b];
       c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
       comm->comm_wait_current();

@@ -44,10 +44,13 @@ static int fin_gpb(int G) { return G <= fin_single() ? std::max(G, 1) : FIN_GPB;
 
 // Per-channel-tile completion counters for the single-launch two-level reductions below
 // (zero-initialised once; the last block of a tile resets its counter, so launches on one stream
-// can reuse them back to back).  One bank of kTileCounters per stream (counter_bank(): up to
-// kCounterBanks streams -- compute, capture, side, warm-up -- before banks are shared), so
+// can reuse them back to back).  One bank of kTileCounters per stream (counter_bank(): the first
+// kCounterBanks distinct streams -- compute, capture, side, warm-up -- get a bank each), so
 // reductions on different streams, e.g. a graph replay beside eager work, never share a counter.
-// Within a bank, forward finalize uses [0, 2048) and backward reduce [2048, 4096).
+// A stream seen after the banks are used up gets NO bank (-1): its reductions take the two-launch
+// path (partials, then finalize), which needs no counter at all.  Sharing a bank between two
+// streams would let concurrent launches count each other's blocks (early or never-completing
+// handshake).  Within a bank, forward finalize uses [0, 2048) and backward reduce [2048, 4096).
 constexpr int kTileCounters = 4096;
 constexpr int kCounterBanks = 8;
 __device__ unsigned int g_tile_counters[kCounterBanks * kTileCounters];
@@ -57,10 +60,17 @@ static int counter_bank(hipStream_t st) {
   static std::unordered_map<hipStream_t, int> banks;
   std::lock_guard<std::mutex> lock(mu);
   auto it = banks.find(st);
-  if (it != banks.end()) return it->second * kTileCounters;
-  const int b = (int)(banks.size() % kCounterBanks);
+  if (it != banks.end()) return it->second < 0 ? -1 : it->second * kTileCounters;
+  const int b = banks.size() < (size_t)kCounterBanks ? (int)banks.size() : -1;
   banks.emplace(st, b);
-  return b * kTileCounters;
+  return b < 0 ? -1 : b * kTileCounters;
+}
+
+// Test introspection: the bank (0..kCounterBanks-1) a stream's single-launch reductions use, or -1
+// when it got none and runs the two-launch path.  Registers the stream like a launch would.
+int bn_counter_bank(hipStream_t st) {
+  const int off = counter_bank(st);
+  return off < 0 ? -1 : off / kTileCounters;
 }
 
 // PDT_BN_LASTBLOCK=0: two launches (partials, then finalize) instead of the last-block handshake
@@ -192,10 +202,11 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
   int P = ceil_div(ngroups, gpb);
   float* ws = out + 4 * (int64_t)K;
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn_finalize: too many channels");
-  if (bn_lastblock()) {
+  const int bank = (bn_lastblock() && P > 1) ? counter_bank(st) : 0;
+  if (bn_lastblock() && bank >= 0) {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
                        ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 0, P,
-                       P > 1 ? counter_bank(st) : 0, gpb);
+                       bank, gpb);
   } else {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part,
                        ngroups, grows, M, K, ws, rm, rv, gamma, beta, momentum, eps, out, 1, P, 0, gpb);
@@ -689,9 +700,10 @@ void launch_bn_bwd_part_reduce(const float* part, int G, int K, float* ws, float
   const int gpb = fin_gpb(G);
   const int P = ceil_div(G, gpb);
   if (ceil_div(K, FIN_CH) > kTileCounters / 2) throw std::runtime_error("bn reduce: too many channels");
-  if (bn_lastblock()) {
+  const int bank = (bn_lastblock() && P > 1) ? counter_bank(st) : 0;
+  if (bn_lastblock() && bank >= 0) {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
-                       sums, invstd, dgamma, dbeta, 0, P, P > 1 ? counter_bank(st) : 0, gpb);
+                       sums, invstd, dgamma, dbeta, 0, P, bank, gpb);
   } else {
     hipLaunchKernelGGL(bn_bwd_part_kernel, dim3(ceil_div(K, FIN_CH), P), dim3(256), 0, st, part, G, K, ws,
                        sums, invstd, dgamma, dbeta, 1, P, 0, gpb);

@@ -90,6 +90,8 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
 // scale, shift; updates running stats in place (unbiased var) when rm/rv non-null.
 // `out` must have room for 4*K + 3*K*bn_finalize_partitions(ngroups) floats (stage-1 scratch).
 int bn_finalize_partitions(int ngroups);
+// completion-counter bank of a stream's single-launch BN reductions, -1 = two-launch path
+int bn_counter_bank(hipStream_t st);
 void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K, float* rm, float* rv,
                         const float* gamma, const float* beta, float momentum, float eps,
                         float* out, hipStream_t st);

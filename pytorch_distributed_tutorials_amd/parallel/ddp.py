@@ -141,7 +141,8 @@ class DistributedDataParallel(nn.Module):
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  comm: str = "auto", wire_dtype: str = "fp32", average: bool = True,
-                 last_bucket_mb: Optional[float] = None, force_reducer: bool = False):
+                 last_bucket_mb: Optional[float] = None, force_reducer: bool = False,
+                 comm_options: Optional["pcomm.CommOptions"] = None):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -189,28 +190,28 @@ class DistributedDataParallel(nn.Module):
         self.buffer_flats = flatten_buffers(module)
 
         # ---- communicator
+        # Every rank takes the same path -- native RCCL on all ranks or on none -- and no rank
+        # enters the RCCL init unless all agreed to (parallel/comm.py: agreement through the
+        # store with a deadline, then a non-blocking init with a deadline).  A rank that cannot
+        # build it makes all ranks fall back (comm='auto') or all raise (comm='rccl'); a rank
+        # that never shows up makes the others raise after the timeout instead of hanging.
         self.comm = None
         be = pcomm.backend_name(process_group)
         single = be == "none" and self.force_reducer  # no process group: world-1 RCCL comm
-        use_native = (comm in ("auto", "rccl") and self.device.type == "cuda"
-                      and (be == "nccl" or single) and native_available())
-        if comm == "rccl" and not use_native:
+        wants = comm in ("auto", "rccl") and (be == "nccl" or single) and self.device.type == "cuda"
+        if comm == "rccl" and not (wants and native_available()):
             raise RuntimeError("comm='rccl' needs a CUDA device, the nccl backend (or force_reducer "
                                "in a single process) and the native extension")
-        if self._collective and use_native:
+        self.comm_options = comm_options or pcomm.CommOptions.from_env()
+        if self._collective and wants:
             try:
-                self.comm = pcomm.native_comm(self.device, process_group)
-            except RuntimeError as e:
+                self.comm = pcomm.native_comm(self.device, process_group, self.comm_options)
+            except pcomm.CommSetupError as e:
+                # the agreement said "not on every rank": a consistent decision on all ranks
+                # (CommSetupTimeout -- a peer never showed up -- is not caught: it ends the run)
                 if comm == "rccl":
                     raise
-                warnings.warn(f"native RCCL communicator unavailable ({e}); gradients are reduced "
-                              "through torch.distributed collectives instead")
-            if self.world_size > 1 and comm != "rccl":
-                # every rank must take the same path: native on all or on none
-                ok = torch.tensor([0 if self.comm is None else 1], dtype=torch.int32, device=self.device)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=process_group)
-                if int(ok.item()) == 0:
-                    self.comm = None
+                warnings.warn(f"{e}; gradients are reduced through torch.distributed collectives")
         # the buffer-broadcast wait can move to the first BatchNorm only where every buffer
         # reader is one of our BN kernels (ops.buffers_ready): the native device model
         self._defer_buffer_wait = (self.comm is not None and getattr(module, "impl", None) == "native"

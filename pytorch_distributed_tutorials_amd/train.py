@@ -30,6 +30,7 @@ from .data import DeviceLoader, DistributedSampler, build_dataset
 from .models import build_model
 from .optim import SGD
 from .parallel import DistributedDataParallel, destroy, init_distributed
+from .parallel.comm import CommOptions
 from .utils.checkpoint import load_checkpoint, save_checkpoint
 from .utils import trace
 from .utils.metrics import StepTimer
@@ -86,8 +87,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--steps", type=int, default=None, help="stop after this many training steps in total")
     p.add_argument("--trace", action="store_true",
                    help="emit roctx ranges (fwd/bwd/step/eval) for rocprofv3 --marker-trace")
-    p.add_argument("--watchdog-timeout", type=float, default=0.0,
-                   help="abort this rank when a step makes no progress for N seconds (0 = off)")
+    p.add_argument("--watchdog-timeout", type=float, default=None,
+                   help="abort this rank when it makes no progress for N seconds (default: 900 when "
+                        "world_size > 1, off for a single process; 0 = off)")
     p.add_argument("--deterministic", action=argparse.BooleanOptionalAction, default=True,
                    help="bitwise-reproducible kernels (reference sets cudnn.deterministic=True); "
                         "--no-deterministic enables atomic split-K weight gradients")
@@ -205,19 +207,30 @@ def main(argv: Optional[list] = None) -> int:
     if args.trace:
         trace.enable(True)
 
+    # progress watchdog, armed before the DDP constructor so a peer that dies during the
+    # communicator bring-up is caught too (on by default for multi-process runs)
+    wd_timeout = args.watchdog_timeout
+    if wd_timeout is None:
+        wd_timeout = 900.0 if env.world_size > 1 else 0.0
+    holder = {}
+    watchdog = None
+    if wd_timeout > 0:
+        watchdog = Watchdog(wd_timeout, rank=env.rank,
+                            on_timeout=lambda: holder["ddp"].abort() if "ddp" in holder else None)
+        watchdog.heartbeat("setup")
+
     model = build_model(args.arch, num_classes=args.num_classes, impl=impl).to(device)
     if impl == "native":
         model.set_impl("native")  # re-assert channels_last weights after .to()
     ddp_model = DistributedDataParallel(model, device_ids=[local_rank] if use_cuda else None,
                                         output_device=local_rank if use_cuda else None,
-                                        bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype)
+                                        bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
+                                        comm_options=CommOptions.from_env(timeout=args.timeout))
+    holder["ddp"] = ddp_model
     criterion = ops.CrossEntropyLoss() if impl == "native" else nn.CrossEntropyLoss()
     timer = StepTimer(device, ddp_model)
     if args.log_every:
         ddp_model.enable_comm_timing(True)
-    watchdog = None
-    if args.watchdog_timeout > 0:
-        watchdog = Watchdog(args.watchdog_timeout, rank=env.rank, on_timeout=ddp_model.abort)
     inject = FaultInjector(env.rank)
     optimizer = SGD(ddp_model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
 

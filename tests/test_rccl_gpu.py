@@ -149,6 +149,124 @@ def test_rccl_world1_collectives(gpu, native_ext):
     c.barrier()
 
 
+def _py(code, timeout=120, **env_extra):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, timeout=timeout,
+                          capture_output=True, text=True)
+
+
+def test_rccl_init_times_out_when_peer_never_joins(gpu):
+    # rank 0 of a 2-rank communicator whose rank 1 never calls init: the non-blocking init must
+    # give up at its deadline with a clear error (a blocking ncclCommInitRank would wait forever)
+    code = (
+        "import time, torch\n"
+        "from pytorch_distributed_tutorials_amd.ops import _ext\n"
+        "C = _ext.native()\n"
+        "t0 = time.time()\n"
+        "try:\n"
+        "    C.RcclComm(C.RcclComm.unique_id(), 0, 2, 0, init_timeout=4.0)\n"
+        "    print('BUILT')\n"
+        "except RuntimeError as e:\n"
+        "    print('ERR', round(time.time() - t0, 1), e)\n")
+    r = _py(code, timeout=150)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith(("ERR", "BUILT"))][-1]
+    assert line.startswith("ERR"), line
+    assert "init timed out" in line and "never joined" in line, line
+    assert 3.5 <= float(line.split()[1]) < 60, line
+
+
+def test_rccl_collective_timeout_aborts_and_raises(gpu):
+    # a collective that does not complete within op_timeout (a stalled peer, simulated by a
+    # sleeping host callback on the comm stream: no GPU kernel spins) -> the monitor aborts the
+    # communicator, records the error, and every later call raises it
+    code = (
+        "import time, torch\n"
+        "from pytorch_distributed_tutorials_amd.ops import _ext\n"
+        "C = _ext.native()\n"
+        "c = C.RcclComm(C.RcclComm.unique_id(), 0, 1, 0, init_timeout=30.0, op_timeout=1.0)\n"
+        "x = torch.ones(1024, device='cuda')\n"
+        "c.all_reduce(x, 'sum'); c.synchronize(); assert c.healthy\n"
+        "c.inject_delay(4.0)\n"
+        "time.sleep(2.5)\n"
+        "print('HEALTHY', c.healthy)\n"
+        "print('ERROR', c.error)\n"
+        "try:\n"
+        "    c.all_reduce(x, 'sum'); print('NO_RAISE')\n"
+        "except RuntimeError as e:\n"
+        "    print('RAISED', e)\n"
+        "time.sleep(2.5)\n")
+    r = _py(code)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = r.stdout
+    assert "HEALTHY False" in out, out
+    assert "did not complete within" in out, out
+    assert "RAISED" in out and "unusable" in out, out
+    assert "[rccl] rank 0:" in r.stderr
+
+
+def test_rccl_collective_timeout_exits_process(gpu):
+    # exit_on_error (default when world > 1): the monitor ends the process with the watchdog's
+    # exit code so the launcher's fail-fast tears the job down
+    code = (
+        "import time, torch\n"
+        "from pytorch_distributed_tutorials_amd.ops import _ext\n"
+        "C = _ext.native()\n"
+        "c = C.RcclComm(C.RcclComm.unique_id(), 0, 1, 0, op_timeout=1.0, exit_on_error=True)\n"
+        "c.inject_delay(3.0)\n"
+        "time.sleep(20)\n"
+        "print('STILL_ALIVE')\n")
+    r = _py(code)
+    assert r.returncode == 124, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "STILL_ALIVE" not in r.stdout
+    assert "did not complete within" in r.stderr
+
+
+def test_rccl_channel_bounds(gpu):
+    # the per-communicator RCCL channel knob (ncclConfig_t minCTAs/maxCTAs) is accepted and the
+    # communicator still reduces correctly
+    from pytorch_distributed_tutorials_amd.ops import _ext
+    C = _ext.native()
+    c = C.RcclComm(C.RcclComm.unique_id(), 0, 1, gpu.index, min_channels=4, max_channels=8)
+    x = torch.randn(1 << 16, device=gpu)
+    y = x.clone()
+    c.all_reduce(y, "sum")
+    c.synchronize()
+    assert torch.equal(x, y) and c.healthy and c.init_seconds >= 0
+
+
+def test_bn_counter_banks_never_shared(gpu):
+    # a 9th stream must not share a completion-counter bank with another stream; it
+    # takes the two-launch BN reduction path instead, and the results stay bitwise equal
+    from pytorch_distributed_tutorials_amd.ops import _ext
+    C = _ext.native()
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(12)]
+    banks = [C.bn_counter_bank(s.cuda_stream) for s in streams]
+    used = [b for b in banks if b >= 0]
+    assert len(used) == len(set(used)), banks          # no bank handed out twice
+    assert banks.count(-1) >= 12 - 8                   # streams past the 8 banks get none
+    # a BN finalize over many groups on a bank-less stream equals the same one on a banked stream
+    K, G = 256, 1200
+    part = torch.rand(G, 2, K, device=gpu)
+    gamma = torch.rand(K, device=gpu)
+    beta = torch.rand(K, device=gpu)
+    outs = []
+    banked = [s for s, b in zip(streams, banks) if b >= 0] or [torch.cuda.current_stream(gpu)]
+    for s in (streams[banks.index(-1)], banked[0]):
+        s.wait_stream(torch.cuda.current_stream(gpu))
+        with torch.cuda.stream(s):
+            rm = torch.zeros(K, device=gpu)
+            rv = torch.ones(K, device=gpu)
+            st = C.bn_finalize(part, G * 64, rm, rv, gamma, beta, 0.1, 1e-5)  # > 512 groups: 2-level
+        torch.cuda.current_stream(gpu).wait_stream(s)
+        outs.append((st.clone(), rm.clone(), rv.clone()))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 def test_bench_force_comm_json(gpu, tmp_path):
     out = tmp_path / "b.json"
     env = dict(os.environ)
