@@ -154,6 +154,9 @@ class DistributedDataParallel(nn.Module):
         self.last_bucket_mb = last_bucket_mb
         self.find_unused_parameters = find_unused_parameters  # unused params are zero-filled
         self.average = average
+        if wire_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"wire_dtype must be 'fp32' or 'bf16', got {wire_dtype!r}")
+        self.wire_dtype = wire_dtype
         self.world_size = pcomm.world_size()
         self.rank = pcomm.rank()
         # force_reducer: run the whole collective path (communicator, reducer, bucket
@@ -288,14 +291,23 @@ class DistributedDataParallel(nn.Module):
                 else:
                     self.comm.current_wait_comm()
 
-    # called from the C++ reducer for non-RCCL backends
+    # called from the C++ reducer for non-RCCL backends.  wire_dtype="bf16" is honoured here too
+    # (cast, sum in bf16 on the wire, cast back): the same numerics as the RCCL path's bf16 wire,
+    # so its accuracy at 8 ranks can be measured with gloo on the CPU (tests/test_wire_cpu.py)
     def _py_launch(self, b: int) -> None:
         if self.world_size > 1:
-            self._works.append(dist.all_reduce(self._flats[b], group=self.process_group, async_op=True))
+            f = self._flats[b]
+            if self.wire_dtype == "bf16":
+                w = f.to(torch.bfloat16)
+                self._works.append((dist.all_reduce(w, group=self.process_group, async_op=True), b, w))
+            else:
+                self._works.append((dist.all_reduce(f, group=self.process_group, async_op=True), b, None))
 
     def _py_finalize(self) -> None:
-        for w in self._works:
-            w.wait()
+        for work, b, w in self._works:
+            work.wait()
+            if w is not None:
+                self._flats[b].copy_(w)
         self._works = []
         if self.average and self.world_size > 1:
             self.space.grad_flat.div_(self.world_size)

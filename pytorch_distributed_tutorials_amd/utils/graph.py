@@ -37,6 +37,13 @@ class CapturedStep:
     the right slots.  ``in_phase()`` tells whether the next replay's baked-in slots still match
     the counters (eager work that advanced a ring by other than a multiple of its cycle breaks
     them: capture again).
+
+    Output validity: the graphs share one private memory pool, so graph k+1 may place its
+    output where graph k keeps temporaries; replaying graph k would then overwrite it.  Each
+    graph therefore copies its output (the step's loss) into a static buffer allocated OUTSIDE
+    the pool before capture, and ``__call__`` returns that buffer: the value of replay k stays
+    valid until graph k is replayed again (``period`` calls later) -- copy it if you need it
+    longer (e.g. to accumulate losses on the device over an epoch).
     """
 
     def __init__(self, step_fn: Callable[[], torch.Tensor], warmup: int = 3,
@@ -54,7 +61,7 @@ class CapturedStep:
         self.phase_sig: List[Tuple[int, ...]] = []  # counters (mod cycle) graph k was captured at
         self.delta: Tuple[int, ...] = ()            # counter advance of one step
         self.graphs: List[torch.cuda.CUDAGraph] = []
-        self.outputs: List[torch.Tensor] = []
+        self.outputs: List[torch.Tensor] = []  # static per-graph output buffers (outside the pool)
         self.calls = 0
 
     @property
@@ -68,23 +75,33 @@ class CapturedStep:
         # warm up on a side stream (lazy init, allocator pools, kernel attributes), then capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        probe = None
         with torch.cuda.stream(s):
             for _ in range(self.warmup):
-                self.step_fn()
+                probe = self.step_fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # output buffers: allocated here, before any capture, so they live outside the pool
+        if probe is not None:
+            self.outputs = [torch.empty_like(probe) for _ in range(self.period)]
+        else:  # no eager warm-up: the step returns its loss, an fp32 scalar
+            self.outputs = [torch.empty((), dtype=torch.float32, device=torch.cuda.current_device()) for _ in range(self.period)]
         start = self.ring[0]() if self.ring is not None else ()
         pool = self.pool
-        for _ in range(self.period):
+        for k in range(self.period):
             if self.ring is not None:
                 self.phase_sig.append(self._mod(self.ring[0]()))
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 out = self.step_fn()
+                if out.shape != self.outputs[k].shape or out.dtype != self.outputs[k].dtype:
+                    raise RuntimeError(f"CapturedStep: step output {tuple(out.shape)} {out.dtype} does not "
+                                       f"match the static buffer {tuple(self.outputs[k].shape)} "
+                                       f"{self.outputs[k].dtype}")
+                self.outputs[k].copy_(out)
             if pool is None:
                 pool = g.pool()  # later phases reuse the first graph's private pool
             self.graphs.append(g)
-            self.outputs.append(out)
         if self.ring is not None:
             end = self.ring[0]()
             if len(end) != len(start):
@@ -101,6 +118,8 @@ class CapturedStep:
         return len(cur) == len(self.delta) and self._mod(cur) == self.phase_sig[self.calls % self.period]
 
     def __call__(self) -> torch.Tensor:
+        """Replay the next graph; returns its static output buffer (valid until that same graph
+        is replayed again, ``period`` calls later)."""
         if not self.graphs:
             self.capture()
         k = self.calls % self.period
