@@ -75,6 +75,9 @@ def parse(argv=None):
     p.add_argument("--watchdog-timeout", type=float, default=None,
                    help="abort a rank that makes no progress for N seconds (default 600 when N > 1, "
                         "off for one process; 0 = off): a dead peer ends the run instead of hanging it")
+    p.add_argument("--comm", default="auto", choices=["auto", "rccl", "xgmi"],
+                   help="gradient all-reduce backend for N>1 (native impl): RCCL (auto/rccl) or the "
+                        "direct one-hop xGMI reduce-scatter/all-gather over IPC-mapped peer buffers")
     p.add_argument("--comm-timeout", type=float, default=None,
                    help="native RCCL communicator: init / per-collective timeout in seconds (600)")
     p.add_argument("--rccl-channels", default=None,
@@ -150,7 +153,7 @@ def main(argv=None) -> int:
                                       bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                                       first_bucket_mb=args.first_bucket_mb,
                                       last_bucket_mb=args.last_bucket_mb,
-                                      force_reducer=args.force_comm, comm_options=copts)
+                                      force_reducer=args.force_comm, comm_options=copts, comm=args.comm)
         holder["ddp"] = ddp
         if args.comm_timing:
             ddp.enable_comm_timing(True)
@@ -230,7 +233,7 @@ def main(argv=None) -> int:
     comm = None
     if args.impl == "native":
         info = ddp.bucket_info()
-        comm = {"native_comm": info["native_comm"], "reducer": info["reducer"],
+        comm = {"native_comm": info["native_comm"], "reducer": info["reducer"], "xgmi": info["xgmi"],
                 "buckets_mb": [round(b / 2**20, 2) for b in info["bucket_bytes"]]}
         if args.comm_timing:
             comm["last_step"] = ddp.comm_stats()
@@ -259,7 +262,7 @@ def main(argv=None) -> int:
                        "seq_len": None, "image_size": args.image_size,
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "backend": backend, "shared_device": bool(args.share_device),
-                       "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype,
+                       "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype, "comm_backend": args.comm,
                        "cudnn_benchmark": bool(args.cudnn_benchmark), "graph": bool(args.graph),
                        "deterministic": bool(args.deterministic), "force_comm": bool(args.force_comm),
                        "first_bucket_mb": args.first_bucket_mb, "last_bucket_mb": args.last_bucket_mb,

@@ -19,6 +19,7 @@
 #include <unordered_map>
 
 #include "comm/rccl_comm.h"
+#include "comm/xgmi_comm.h"
 #include "ddp/reducer.h"
 #include "kernels/kernels.h"
 
@@ -1245,12 +1246,36 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("init_seconds", &pdt::RcclComm::init_seconds)
       .def("inject_delay", &pdt::RcclComm::inject_delay, py::arg("seconds"));
 
+  py::class_<pdt::XgmiComm, std::shared_ptr<pdt::XgmiComm>>(m, "XgmiComm")
+      .def(py::init<int, int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("device"), py::arg("numel"), py::arg("nbuckets"), py::arg("timeout") = 600.0)
+      .def_property_readonly("rank", &pdt::XgmiComm::rank)
+      .def_property_readonly("world", &pdt::XgmiComm::world)
+      .def_property_readonly("device", &pdt::XgmiComm::device)
+      .def_property_readonly("numel", &pdt::XgmiComm::numel)
+      .def_property_readonly("stream_ptr",
+                             [](const pdt::XgmiComm& c) { return reinterpret_cast<uintptr_t>(c.stream()); })
+      .def("ipc_handles", [](const pdt::XgmiComm& c) { return py::bytes(c.ipc_handles()); })
+      .def("open_peers", &pdt::XgmiComm::open_peers, py::arg("handles"))
+      .def("link_local", &pdt::XgmiComm::link_local, py::arg("comms"))
+      .def("grad_buffer", &pdt::XgmiComm::grad_buffer)
+      .def("reduce_bucket", &pdt::XgmiComm::reduce_bucket, py::arg("bucket"), py::arg("offset"),
+           py::arg("count"), py::arg("average") = true)
+      .def("reduce_bucket_phases", &pdt::XgmiComm::reduce_bucket_phases, py::arg("bucket"), py::arg("offset"),
+           py::arg("count"), py::arg("average"), py::arg("lo"), py::arg("hi"))
+      .def("comm_wait_current", &pdt::XgmiComm::comm_wait_current)
+      .def("current_wait_comm", &pdt::XgmiComm::current_wait_comm)
+      .def("synchronize", &pdt::XgmiComm::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("error_code", &pdt::XgmiComm::error_code)
+      .def("check", &pdt::XgmiComm::check);
+
   py::class_<pdt::Reducer>(m, "Reducer")
       .def(py::init<std::vector<Tensor>, std::vector<Tensor>, std::vector<int64_t>, std::vector<Tensor>,
-                    std::shared_ptr<pdt::RcclComm>, py::object, py::object, bool, std::string>(),
+                    std::shared_ptr<pdt::RcclComm>, py::object, py::object, bool, std::string,
+                    std::shared_ptr<pdt::XgmiComm>>(),
            py::arg("params"), py::arg("grad_views"), py::arg("bucket_of_param"),
            py::arg("bucket_flats"), py::arg("comm"), py::arg("py_launch"), py::arg("py_finalize"),
-           py::arg("average") = true, py::arg("wire_dtype") = "fp32")
+           py::arg("average") = true, py::arg("wire_dtype") = "fp32", py::arg("xgmi") = nullptr)
       .def("prepare_for_backward", &pdt::Reducer::prepare_for_backward,
            py::call_guard<py::gil_scoped_release>())
       .def("mark_ready_external", &pdt::Reducer::mark_ready_external)

@@ -24,6 +24,8 @@ struct ReducerState {
   std::vector<at::Tensor> flats;
   std::vector<std::vector<int64_t>> members;  // params per bucket
   std::shared_ptr<RcclComm> comm;
+  std::shared_ptr<XgmiComm> xgmi;  // direct xGMI reduce-scatter/all-gather backend (instead of comm)
+  std::vector<int64_t> flat_off;   // per bucket: element offset in the xGMI gradient buffer
   py::object py_launch, py_finalize;
   bool average = true;
   bool wire_bf16 = false;
@@ -71,6 +73,17 @@ struct ReducerState {
   void launch_bucket(int64_t b) {
     const bool first = launch_order.empty();
     launch_order.push_back(b);
+    if (xgmi) {
+      xgmi->check();  // a peer timed out earlier: raise here, out of backward()
+      c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
+      xgmi->comm_wait_current();
+      if (aux) {
+        hipEventRecord(ev_aux, aux);
+        hipStreamWaitEvent(xgmi->stream(), ev_aux, 0);
+      }
+      xgmi->reduce_bucket((int)b, flat_off[b], flats[b].numel(), average);
+      return;
+    }
     if (comm) {
       comm->check();  // a timed-out / failed communicator: raise here, out of backward()
       const at::Tensor& f = flats[b];
@@ -167,7 +180,9 @@ struct ReducerState {
     // parameters that received no gradient this iteration (unused in forward): zero views
     for (size_t i = 0; i < params.size(); ++i)
       if (!param_ready[i]) mark_param((int64_t)i, /*zero_if_missing=*/true);
-    if (comm) {
+    if (xgmi) {
+      xgmi->current_wait_comm();
+    } else if (comm) {
       if (timing) {
         c10::hip::HIPGuard guard((c10::DeviceIndex)comm->device());
         hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)comm->device()).stream();
@@ -190,7 +205,7 @@ struct ReducerState {
 Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
                  std::vector<int64_t> bucket_of_param, std::vector<at::Tensor> bucket_flats,
                  std::shared_ptr<RcclComm> comm, py::object py_launch, py::object py_finalize,
-                 bool average, std::string wire_dtype)
+                 bool average, std::string wire_dtype, std::shared_ptr<XgmiComm> xgmi)
     : st_(std::make_shared<ReducerState>()) {
   if (params.size() != grad_views.size() || params.size() != bucket_of_param.size())
     throw std::runtime_error("Reducer: params/views/bucket_of size mismatch");
@@ -199,6 +214,19 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   st_->bucket_of = std::move(bucket_of_param);
   st_->flats = std::move(bucket_flats);
   st_->comm = std::move(comm);
+  st_->xgmi = std::move(xgmi);
+  if (st_->xgmi) {
+    if (st_->comm) throw std::runtime_error("Reducer: give either the RCCL or the xGMI communicator");
+    if (wire_dtype != "fp32") throw std::runtime_error("Reducer: the xGMI backend reduces fp32 gradients");
+    // every bucket must be a slice of the communicator's shared gradient buffer
+    const float* base = st_->xgmi->grad_buffer().data_ptr<float>();
+    for (const auto& f : st_->flats) {
+      const int64_t off = f.data_ptr<float>() - base;
+      if (!f.is_contiguous() || off < 0 || off + f.numel() > st_->xgmi->numel())
+        throw std::runtime_error("Reducer: bucket is not a slice of the xGMI gradient buffer");
+      st_->flat_off.push_back(off);
+    }
+  }
   st_->py_launch = std::move(py_launch);
   st_->py_finalize = std::move(py_finalize);
   st_->average = average;

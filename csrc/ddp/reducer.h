@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../comm/rccl_comm.h"
+#include "../comm/xgmi_comm.h"
 
 namespace pdt {
 
@@ -41,7 +42,8 @@ class Reducer {
   Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_views,
           std::vector<int64_t> bucket_of_param, std::vector<at::Tensor> bucket_flats,
           std::shared_ptr<RcclComm> comm, pybind11::object py_launch,
-          pybind11::object py_finalize, bool average, std::string wire_dtype);
+          pybind11::object py_finalize, bool average, std::string wire_dtype,
+          std::shared_ptr<XgmiComm> xgmi = nullptr);
   ~Reducer();
 
   void prepare_for_backward();

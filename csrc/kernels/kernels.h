@@ -239,4 +239,16 @@ void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uin
                                 bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
                                 uint8_t* dy8, float* state, int slot, hipStream_t st);
 
+// ---------------------------------------------------------------- xgmi.hip
+// Direct one-hop all-reduce of elements [lo, lo + count) of every rank's fp32 gradient buffer
+// (bucket `bucket`, epoch `epoch`): signal ready -> wait (bounded) -> reduce own shard from all
+// peers -> signal reduced -> wait -> gather every shard back (divided by world when `average`).
+// g / red / flags: device pointers of every rank's buffers as mapped in this process; err: device
+// view of a host word set to a nonzero code when a wait passes timeout_ticks (wall clock).
+int xgmi_max_ranks();
+void launch_xgmi_bucket(const float* const* g, const float* const* red, unsigned* const* flags, int world,
+                        int rank, int bucket, int64_t lo, int64_t count, unsigned epoch, bool average,
+                        uint64_t timeout_ticks, unsigned* err, hipStream_t st, int phase_lo = 0,
+                        int phase_hi = 5);
+
 }  // namespace pdt

@@ -180,7 +180,23 @@ class DistributedDataParallel(nn.Module):
         sizes = [p.numel() * p.element_size() for p in params]
         plan = ddp_bucket_plan(sizes, self.bucket_cap_mb, self.first_bucket_mb, self.last_bucket_mb)
         layout = [i for b in plan for i in b]
-        self.space = FlatParamSpace([params[i] for i in layout])
+        self.comm_options = comm_options or pcomm.CommOptions.from_env()
+        # comm="xgmi": the flat gradient buffer is the IPC-shared buffer of the direct xGMI
+        # all-reduce (parallel/xgmi.py); buckets are reduced by one-hop reduce-scatter/all-gather
+        # kernels over every peer link instead of RCCL rings
+        self.xgmi = None
+        grad_storage = None
+        if comm == "xgmi":
+            if self.device.type != "cuda" or not native_available():
+                raise RuntimeError("comm='xgmi' needs a GPU device and the native extension")
+            if wire_dtype != "fp32":
+                raise ValueError("comm='xgmi' reduces fp32 gradients (wire_dtype='fp32')")
+            from .xgmi import xgmi_comm
+            self._collective = True
+            self.xgmi = xgmi_comm(self.device, sum(p.numel() for p in params), len(plan), process_group,
+                                  timeout=self.comm_options.init_timeout)
+            grad_storage = self.xgmi.grad_buffer()
+        self.space = FlatParamSpace([params[i] for i in layout], grad_flat=grad_storage)
         self.bucket_ranges = []
         pos = 0
         for b in plan:
@@ -205,7 +221,6 @@ class DistributedDataParallel(nn.Module):
         if comm == "rccl" and not (wants and native_available()):
             raise RuntimeError("comm='rccl' needs a CUDA device, the nccl backend (or force_reducer "
                                "in a single process) and the native extension")
-        self.comm_options = comm_options or pcomm.CommOptions.from_env()
         if self._collective and wants:
             try:
                 self.comm = pcomm.native_comm(self.device, process_group, self.comm_options)
@@ -237,7 +252,7 @@ class DistributedDataParallel(nn.Module):
                 self.reducer = native().Reducer(
                     sp.params, sp.grad_views, bucket_of, flats, self.comm,
                     self._py_launch, self._py_finalize, self.average,
-                    wire_dtype if self.comm is not None else "fp32")
+                    wire_dtype if self.comm is not None else "fp32", xgmi=self.xgmi)
             else:
                 self.reducer = _PyReducer(sp.params, sp.grad_views, bucket_of, flats,
                                           self._py_launch, self._py_finalize)
@@ -365,4 +380,5 @@ class DistributedDataParallel(nn.Module):
         return {"num_buckets": len(self.bucket_ranges), "bucket_elems": list(self.bucket_sizes),
                 "bucket_bytes": list(self.bucket_bytes),
                 "native_comm": self.comm is not None, "forced": self.force_reducer,
+                "xgmi": self.xgmi is not None,
                 "reducer": type(self.reducer).__name__ if self.reducer is not None else None}

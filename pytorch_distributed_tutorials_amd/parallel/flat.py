@@ -30,7 +30,9 @@ _VERSION = operator.attrgetter("_version")
 
 
 class FlatParamSpace:
-    def __init__(self, params: Sequence[torch.nn.Parameter]):
+    def __init__(self, params: Sequence[torch.nn.Parameter], grad_flat: Optional[torch.Tensor] = None):
+        """``grad_flat``: caller-provided storage for the flat gradient buffer (e.g. the IPC-shared
+        buffer of the xGMI all-reduce backend); zeroed here."""
         if not params:
             raise ValueError("FlatParamSpace needs at least one parameter")
         dev, dt = params[0].device, params[0].dtype
@@ -48,7 +50,15 @@ class FlatParamSpace:
         self.numel = off
         self.device, self.dtype = dev, dt
         self.param_flat = torch.empty(off, device=dev, dtype=dt)
-        self.grad_flat = torch.zeros(off, device=dev, dtype=dt)
+        if grad_flat is None:
+            self.grad_flat = torch.zeros(off, device=dev, dtype=dt)
+        else:
+            if grad_flat.numel() != off or grad_flat.dtype != dt or grad_flat.device != dev \
+                    or not grad_flat.is_contiguous():
+                raise ValueError("grad_flat must be a contiguous tensor of the space's size, dtype and device")
+            self.grad_flat = grad_flat
+            with torch.no_grad():
+                self.grad_flat.zero_()
         self.grad_views: List[torch.Tensor] = []
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.reducer = None  # set by DistributedDataParallel when gradients are all-reduced
