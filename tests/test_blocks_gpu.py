@@ -10,10 +10,14 @@ distinct ResNet-50 Bottleneck and ResNet-18 BasicBlock configuration at batch 32
 spatial size of its stage (224 px input), and compare with the same blocks in fp32 torch from
 identical weights and input:
 
-* output, input gradient, every conv weight / BN gamma / BN beta gradient, running mean / var:
-  relative L2 error < 2e-2 (bf16 activations and operands, fp32 accumulation);
-* and no worse than 1.5x stock autocast-bf16 on the same blocks where that is the larger
-  (the bf16 noise yardstick).
+* output and running mean / var: relative L2 error < 2e-2 (bf16 activations and operands, fp32
+  accumulation); measured 5.6e-3 - 8.1e-3 for the outputs;
+* input gradient and every conv weight / BN gamma / BN beta gradient: < 2e-2, or no worse than
+  1.5x stock autocast-bf16 on the same blocks where that is larger.  With a random upstream
+  gradient, bf16 rounding flips ReLU decisions for pre-activations within an ulp of zero (~0.3 % of
+  them), and each flip moves that element's gradient by its full size: ~5-13 % relative L2 against
+  fp32 for ANY bf16 implementation -- autocast measures 4.8e-2 - 1.2e-1 on these tensors, ours
+  1.0-1.2x that (profiles/r3_numerics.md has every case).
 
 Each stage is tested as its first two blocks chained (stride-2 / projection block, then an
 identity block), so the block-to-block BN hand-off is exercised at every width.
@@ -135,5 +139,7 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw):
     if os.environ.get("PDT_REPORT_DIR"):  # GPU runs keep the measured errors (profiles/)
         with open(os.path.join(os.environ["PDT_REPORT_DIR"], "block_numerics.txt"), "a") as f:
             f.write(line + "\n")
-    bad = {k: (round(v, 5), round(yard[k], 5)) for k, v in errs.items() if v > max(TOL, 1.5 * yard[k])}
+    strict = lambda k: k == "out" or "running" in k  # noqa: E731 -- no ReLU-flip noise in these
+    bad = {k: (round(v, 5), round(yard[k], 5)) for k, v in errs.items()
+           if v > (TOL if strict(k) else max(TOL, 1.5 * yard[k]))}
     assert not bad, bad

@@ -860,3 +860,71 @@ def test_avgpool_linear_and_ce_autograd(gpu, native_ext):
     assert abs(loss.item() - lr.item()) < 1e-2 * lr.item()
     assert _rel_err(w.grad, wr.grad) < 1e-2 and _rel_err(b.grad, br.grad) < 1e-2
     assert _rel_err(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 64, 96), (2, 62, 250), (1, 40, 300)])
+def test_stem_halo_conv_vs_fp32(gpu, native_ext, n, h, w):
+    """Halo-staged stem forward (csrc/kernels/stem.hip) vs fp32 conv2d on the same bf16-rounded
+    image and weights, plus its per-output-row BN partials (sum, M2) vs fp32; the Wo > 128 case
+    falls back to the generic implicit GEMM (row-tile partials)."""
+    C = native_ext
+    torch.manual_seed(1)
+    x = torch.randn(n, 3, h, w, device=gpu)
+    wt = (torch.randn(64, 3, 7, 7, device=gpu) * 0.1).contiguous(memory_format=torch.channels_last)
+    xsp, y, part, grows = C.stem_conv_fwd(x, wt, 2, 3, True)
+    ref = torch.nn.functional.conv2d(x.bfloat16().float(), wt.bfloat16().float(), stride=2, padding=3)
+    ho, wo = ref.shape[2], ref.shape[3]
+    assert y.shape == (n, ho, wo, 64)
+    assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+    rows = ref.permute(0, 2, 3, 1).reshape(-1, 64)  # [N*Ho*Wo, K] in NHWC row order
+    assert grows == (wo if wo <= 128 else grows)
+    g = part.shape[0]
+    assert g == (rows.shape[0] + grows - 1) // grows
+    pad = g * grows - rows.shape[0]
+    rr = torch.cat([rows, rows.new_full((pad, 64), float("nan"))]).view(g, grows, 64)
+    cnt = (~rr.isnan()).sum(1).float()
+    s = torch.nansum(rr, 1)
+    mean = s / cnt
+    m2 = torch.nansum((rr - mean[:, None, :]) ** 2, 1)
+    assert _rel_err(part[:, 0], s) < 1e-2
+    assert _rel_err(part[:, 1], m2) < 1e-2
+
+
+@pytest.mark.parametrize("det", [False, True])
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 64, 96)])
+def test_stem_bwd_fused_matches_unfused(gpu, native_ext, n, h, w, det):
+    """Fused stem backward (BN/pool apply inside the weight gradient, csrc/kernels/stem.hip) vs the
+    unfused pool_bn_bwd_apply + stem_wgrad on identical inputs (same bf16 dy values, different
+    summation order), and vs an fp32 reference weight gradient of the same bf16 dy."""
+    C = native_ext
+    torch.manual_seed(2)
+    x = torch.randn(n, 3, h, w, device=gpu)
+    wt = (torch.randn(64, 3, 7, 7, device=gpu) * 0.1).contiguous(memory_format=torch.channels_last)
+    xsp, y, part, grows = C.stem_conv_fwd(x, wt, 2, 3, True)
+    gamma = torch.rand(64, device=gpu) + 0.5
+    beta = torch.rand(64, device=gpu) - 0.5
+    rm, rv = torch.zeros(64, device=gpu), torch.ones(64, device=gpu)
+    cnt = y.shape[0] * y.shape[1] * y.shape[2]
+    stats = C.bn_finalize(part, cnt, rm, rv, gamma, beta, 0.1, 1e-5, grows)
+    pooled, idx = C.bn_relu_maxpool(y, stats[2], stats[3])
+    dpool = torch.randn(pooled.shape, device=gpu).bfloat16()
+    sums = C.pool_bn_bwd_reduce(dpool, idx, y, stats)
+    dy = C.pool_bn_bwd_apply(dpool, idx, y, stats, gamma, sums, True)
+    ref = C.stem_wgrad(dy, xsp, [64, 3, 7, 7], det)
+    got = C.stem_bwd_fused(dpool, idx, y, stats, gamma, sums, True, xsp, [64, 3, 7, 7], det)
+    torch.cuda.synchronize()
+    assert _rel_err(got, ref) < 1e-3
+    # fp32 reference: weight gradient of the same (bf16) dy on the bf16 image
+    xb = x.bfloat16().float().requires_grad_(False)
+    w32 = wt.bfloat16().float().requires_grad_(True)
+    yy = torch.nn.functional.conv2d(xb, w32, stride=2, padding=3)
+    yy.backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel_err(got, w32.grad) < 1e-2
+    if det:  # deterministic slabs: bitwise repeatable
+        again = C.stem_bwd_fused(dpool, idx, y, stats, gamma, sums, True, xsp, [64, 3, 7, 7], det)
+        assert torch.equal(got, again)
+    # eval-mode apply (k1 * g only)
+    dy_e = C.pool_bn_bwd_apply(dpool, idx, y, stats, gamma, sums, False)
+    ref_e = C.stem_wgrad(dy_e, xsp, [64, 3, 7, 7], det)
+    got_e = C.stem_bwd_fused(dpool, idx, y, stats, gamma, sums, False, xsp, [64, 3, 7, 7], det)
+    assert _rel_err(got_e, ref_e) < 1e-3

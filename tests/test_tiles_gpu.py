@@ -236,11 +236,16 @@ def test_resnet50_112px_matches_fp32_torch(gpu, native_ext):
     if os.environ.get("PDT_REPORT_DIR"):
         with open(os.path.join(os.environ["PDT_REPORT_DIR"], "resnet50_stage_cosines.txt"), "a") as f:
             f.write(f"train {report} global {cos_n:.4f}/{cos_b:.4f}\n")
-    # the head and the last stage are pinned absolutely (their gradients are not yet washed out by
-    # the train-mode BN cancellation chain); every stage is pinned relative to stock autocast bf16
-    for k in ("layer4", "fc"):
-        assert st[k][0] > 0.9, (k, st[k], report)
-    for k, (cn, cb) in st.items():
+    # Measured on MI355X (profiles/r3_numerics.md): per-stage cosines native/autocast fc 0.984/0.984,
+    # layer4 0.40/0.40, layer3 0.20/0.20, layer2 0.17/0.16, layer1 0.16/0.15, conv1 0.14/0.16 -- bf16
+    # ReLU-mask flips (pre-activations within a bf16 ulp of zero) decorrelate a random-init train-mode
+    # gradient more with every stage it crosses, for ANY bf16 implementation.  So the head is pinned
+    # absolutely and every conv stage relative to stock autocast bf16 on the same weights.  (The stem
+    # BN's 128 parameters are excluded: their direction is noise for both, cosines -0.15 / -0.06.)
+    assert st["fc"][0] > 0.97, (st["fc"], report)
+    assert st["layer4"][0] > 0.3, (st["layer4"], report)
+    for k in ("conv1", "layer1", "layer2", "layer3", "layer4", "fc"):
+        cn, cb = st[k]
         assert cn > cb - 0.05, (k, cn, cb, report)
     for (name, bt), (_, bn) in zip(mt.named_buffers(), mn.named_buffers()):
         if bt.dtype == torch.int64:

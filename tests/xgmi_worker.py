@@ -69,6 +69,8 @@ def run_ddp(rank, world, dev):
     from pytorch_distributed_tutorials_amd import ops
     from pytorch_distributed_tutorials_amd.models import build_model
     from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_tutorials_amd.utils.seed import set_random_seeds
+    set_random_seeds(0, deterministic=True)  # slab split-K weight gradients: bitwise repeatable
     torch.manual_seed(0)
     base = build_model("resnet18", num_classes=10).to(dev)
     gen = torch.Generator().manual_seed(50 + rank)
