@@ -410,8 +410,17 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
 // -------------------------------------------------------------------- stem
 // 7x7/s2 stem with C <= 4 input channels as a super-pixel conv (kernels.h): returns
 // (xsp, y, part) -- xsp is the bf16 super-pixel image (kept for the weight gradient)
-std::tuple<Tensor, Tensor, Tensor> stem_conv_fwd(const Tensor& x, const Tensor& w, int64_t stride,
-                                                 int64_t pad, bool stats) {
+static bool stem_halo_mode() {  // PDT_STEM_HALO=0: the generic super-pixel implicit GEMM (A/B knob)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_STEM_HALO");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+std::tuple<Tensor, Tensor, Tensor, int64_t> stem_conv_fwd(const Tensor& x, const Tensor& w, int64_t stride,
+                                                          int64_t pad, bool stats) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "stem: image must be fp32 NCHW");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4, "stem: weight must be fp32 4-D");
   TORCH_CHECK(stride == 2 && x.size(1) <= 4 && w.size(1) == x.size(1), "stem: stride 2, <= 4 channels");
@@ -435,14 +444,17 @@ std::tuple<Tensor, Tensor, Tensor> stem_conv_fwd(const Tensor& x, const Tensor& 
   auto y = at::empty({N, Ho, Wo, K}, xsp.options());
   Tensor part;
   float* pp = nullptr;
+  const int M = N * Ho * Wo;
+  const bool halo = stem_halo_mode() && pdt::stem_halo_supported(K, R, Sp, Wo);
+  // BN partial groups: one per output row on the halo kernel, one per NT row tile otherwise
+  const int grows = halo ? Wo : pdt::conv_nt_group_rows(M, K, R * Sp * 8 * 2);
   if (stats) {
-    const int M = N * Ho * Wo;
-    const int grows = pdt::conv_nt_group_rows(M, K, R * Sp * 8 * 2);
     part = at::empty({(M + grows - 1) / grows, 2, K}, x.options());
     pp = part.data_ptr<float>();
   }
-  pdt::launch_conv_fwd(cbf(xsp), cbf(wsp), bf(y), pp, s, st);
-  return {xsp, y, part};
+  if (halo) pdt::launch_stem_conv_fwd(cbf(xsp), cbf(wsp), bf(y), pp, N, Hp, Wsp, Ho, Wo, st);
+  else pdt::launch_conv_fwd(cbf(xsp), cbf(wsp), bf(y), pp, s, st);
+  return {xsp, y, part, (int64_t)grows};
 }
 
 // weight gradient of the stem from the super-pixel image; accumulates into `out` (fp32 [K,C,R,S],
@@ -481,16 +493,65 @@ Tensor stem_wgrad(const Tensor& dy, const Tensor& xsp, std::vector<int64_t> wsz,
   return o;
 }
 
+// stem backward with the BN/pool apply fused into the weight gradient: accumulates dW into `out`
+// (fp32 [K,C,R,S], any strides) when given, else returns a fresh channels_last tensor
+Tensor stem_bwd_fused(const Tensor& dpool, const Tensor& idx, const Tensor& y, const Tensor& stats,
+                      const Tensor& gamma, const Tensor& sums, bool training, const Tensor& xsp,
+                      std::vector<int64_t> wsz, bool deterministic, const std::optional<Tensor>& out) {
+  check_bf16_nhwc(dpool, "dpool");
+  check_bf16_nhwc(y, "y");
+  check_bf16_nhwc(xsp, "xsp");
+  TORCH_CHECK(wsz.size() == 4, "weight shape must be [K,C,R,S]");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() &&
+              idx.numel() == dpool.numel(), "idx: uint8 argmax map like dpool");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.numel() == 4 * y.size(3) &&
+              sums.scalar_type() == at::kFloat && sums.numel() == 2 * y.size(3), "stats [4][K], sums [2][K]");
+  c10::hip::HIPGuard g(y.get_device());
+  const int K = wsz[0], C = wsz[1], R = wsz[2], S = wsz[3];
+  const int Sp = (S + 2) / 2;
+  const int N = y.size(0), Ho = y.size(1), Wo = y.size(2);
+  TORCH_CHECK(y.size(3) == K && pdt::stem_bwd_fused_supported(K, R, Sp, Ho, Wo), "stem_bwd_fused: unsupported shape");
+  TORCH_CHECK(dpool.size(0) == N && dpool.size(1) == Ho / 2 && dpool.size(2) == Wo / 2 && dpool.size(3) == K,
+              "stem_bwd_fused: dpool must be the 3x3/s2/p1 max pool of y");
+  TORCH_CHECK(xsp.size(0) == N && xsp.size(2) == Wo + Sp - 1 && xsp.size(3) == 8, "stem_bwd_fused: xsp shape");
+  auto fopt = y.options().dtype(at::kFloat);
+  auto dwsp = at::empty({K, R, Sp, 8}, fopt);
+  Tensor wsb;
+  if (deterministic) wsb = at::empty({(int64_t)pdt::stem_bwd_fused_blocks(N, Ho) * K * R * Sp * 8}, fopt);
+  hipStream_t st = cur_stream(y);
+  pdt::launch_stem_bwd_fused(cbf(dpool), idx.data_ptr<uint8_t>(), cbf(y), stats.data_ptr<float>(),
+                             gamma.data_ptr<float>(), sums.data_ptr<float>(), training, cbf(xsp), N, Ho, Wo,
+                             xsp.size(1), xsp.size(2), dwsp.data_ptr<float>(),
+                             deterministic ? wsb.data_ptr<float>() : nullptr, st);
+  Tensor o;
+  bool acc = false;
+  if (out.has_value() && out->defined()) {
+    o = *out;
+    TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
+                o.size(2) == R && o.size(3) == S, "stem_bwd_fused out: bad shape/dtype");
+    acc = true;
+  } else {
+    o = at::empty({K, C, R, S}, fopt.memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  int64_t os[4] = {o.stride(0), o.stride(1), o.stride(2), o.stride(3)};
+  pdt::launch_stem_wgrad_unpack(dwsp.data_ptr<float>(), o.data_ptr<float>(), os, K, C, R, S, Sp, acc, st);
+  return o;
+}
+
 // ---------------------------------------------------------------------- BN
 Tensor bn_finalize(const Tensor& part, int64_t count, const Tensor& rm, const Tensor& rv,
-                   const Tensor& gamma, const Tensor& beta, double momentum, double eps) {
+                   const Tensor& gamma, const Tensor& beta, double momentum, double eps, int64_t grows_in) {
   check_cuda(part, "part");
   c10::hip::HIPGuard g(part.get_device());
   int ng = part.size(0), K = part.size(2);
   // the producing conv's row group is its NT tile's BM (64, 128 or 256; conv_nt_group_rows): the
-  // only one of those giving ng groups over `count` rows; a single group covers every row
+  // only one of those giving ng groups over `count` rows; a single group covers every row.  A
+  // producer with another grouping (the halo stem: one group per output row) passes grows_in.
   int grows = 0;
-  if (ng == 1) {
+  if (grows_in > 0) {
+    TORCH_CHECK((count + grows_in - 1) / grows_in == ng, "bn_finalize: grows does not match the partials");
+    grows = (int)grows_in;
+  } else if (ng == 1) {
     grows = (int)count;
   } else {
     for (int g : {64, 128, 256})
@@ -1122,7 +1183,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("stats"));
   m.def("stem_wgrad", checked("stem_wgrad", &stem_wgrad), py::arg("dy"), py::arg("xsp"),
         py::arg("w_shape"), py::arg("deterministic") = false, py::arg("out") = py::none());
-  m.def("bn_finalize", checked("bn_finalize", &bn_finalize));
+  m.def("stem_bwd_fused", checked("stem_bwd_fused", &stem_bwd_fused), py::arg("dpool"), py::arg("idx"),
+        py::arg("y"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("training"), py::arg("xsp"),
+        py::arg("w_shape"), py::arg("deterministic") = false, py::arg("out") = py::none());
+  m.def("stem_bwd_fused_supported", &pdt::stem_bwd_fused_supported, py::arg("K"), py::arg("R"), py::arg("Sp"),
+        py::arg("Ho"), py::arg("Wo"));
+  m.def("bn_finalize", checked("bn_finalize", &bn_finalize), py::arg("part"), py::arg("count"), py::arg("rm"),
+        py::arg("rv"), py::arg("gamma"), py::arg("beta"), py::arg("momentum"), py::arg("eps"),
+        py::arg("grows") = 0);
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"), py::arg("res_scale") = py::none(),

@@ -29,6 +29,21 @@ size_t pack_t_entry_bytes();
 void launch_stem_image(const float* x, uint16_t* xsp, int N, int C, int H, int W, int pad, int Hp,
                        int Wsp, hipStream_t st);
 // wsp[k][r][p][q*4+c] = w[k][c][r][2p+q-1] (0 outside), w fp32 with strides
+// Halo-staged stem forward (stem.hip): y[N][Ho][Wo][64] = conv(xsp, wsp) with K = 64, R = 7,
+// Sp = 4 super-pixel taps, stride (2, 1); part (optional) = BN partials [N*Ho][2][64], one group
+// per output row (Wo rows each).  Supported when stem_halo_supported(K, R, Sp, Wo).
+bool stem_halo_supported(int K, int R, int Sp, int Wo);
+void launch_stem_conv_fwd(const uint16_t* xsp, const uint16_t* wsp, uint16_t* y, float* part, int N, int Hp,
+                          int Wsp, int Ho, int Wo, hipStream_t st);
+// Fused stem backward (stem.hip): dwsp[64][7][4][8] (fp32) = weight gradient of the super-pixel
+// stem conv for dy = BN-backward-apply(maxpool_bwd(dpool, idx)) computed on the fly (ReLU mask from
+// y, training-mode or eval apply with stats [4][64], gamma, sums [2][64]).  ws: null (fp32 atomics)
+// or stem_bwd_fused_blocks(N, Ho) * 64 * 224 floats (deterministic slabs).
+bool stem_bwd_fused_supported(int K, int R, int Sp, int Ho, int Wo);
+int stem_bwd_fused_blocks(int N, int Ho);
+void launch_stem_bwd_fused(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y, const float* stats,
+                           const float* gamma, const float* sums, bool training, const uint16_t* xsp, int N,
+                           int Ho, int Wo, int Hp, int Wsp, float* dwsp, float* ws, hipStream_t st);
 void launch_stem_pack_weight(const float* w, const int64_t* strides, uint16_t* wsp, int K, int C,
                              int R, int S, int Sp, hipStream_t st);
 // out[k][c][r][s] (+)= dwsp[k][r][(s+1)/2][((s+1)%2)*4+c], out channels_last (strides k:CRS... given)

@@ -1,0 +1,444 @@
+// ResNet stem forward (7x7 / stride 2 / pad 3, 3 input channels -> 64) as a halo-staged implicit
+// GEMM on the bf16 MFMA.
+//
+// The image is first re-laid out as "super-pixels" (layout.hip, launch_stem_image): pairs of
+// horizontally adjacent pixels form one 8-channel pixel, so the 7x7/s2 filter becomes 7 rows x 4
+// super-pixel taps of 8 channels, stride (2, 1): K_gemm = 7*4*8 = 224.  The generic NT kernel
+// gathers that im2col matrix through LDS-DMA one 16-byte tap at a time: every input super-pixel is
+// fetched ~14 times (7 rows x 4 taps / stride 2), about 2 GB of L2->LDS traffic per step at batch
+// 256, and the stem ran at 267 us against a ~95 us HBM floor (profiles/r3a_step_calls.txt).
+//
+// Here a workgroup of ROWS waves owns ROWS consecutive output rows of one image (wave w = row
+// ho0 + w, all Wo pixels, all 64 channels).  It stages ONCE the 2*ROWS+5 input super-pixel rows
+// those outputs read -- one contiguous span of the image, copied by LDS-DMA -- plus the packed
+// weights, and every tap's MFMA operand is a shifted ds_read_b128 view of the staged rows:
+//   B operand (pixels): lane (pixel fr, k-group fq) of tap row r reads super-pixel (2w + r, wo + fq)
+//   A operand (weights): lane (channel fr, k-group fq) reads wsp[ch][r][fq][0..7]
+// so K-step r (32 of K) is one filter row, k-group fq one super-pixel tap.  Consecutive pixels of
+// a fragment read consecutive 16-byte LDS slots (conflict-free); the weight image is padded to a
+// 464-byte row pitch, which spreads its 16 fragment rows over 16 distinct slots.
+//
+// Epilogue: BN statistics per output row (sum and M2 about the row mean, two passes over the
+// fp32 accumulators -- no cancellation), one partial group per (image, output row), and the bf16
+// output written as 8-byte channel quads.
+#include "common.h"
+#include "kernels.h"
+#include "pool_quad.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace pdt {
+
+namespace {
+
+constexpr int STEM_K = 64;          // output channels
+constexpr int STEM_R = 7;           // filter rows
+constexpr int STEM_SP = 4;          // super-pixel taps per row
+constexpr int STEM_ROWS = 4;        // output rows (= waves) per workgroup
+constexpr int W_PITCH = 464;        // bytes per packed weight row in LDS (448 + 16 pad)
+constexpr int W_BYTES = STEM_K * W_PITCH;
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)(reinterpret_cast<uintptr_t>(lds)), 16, voff, 0, 0, 0);
+}
+
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ v4f mfma16(const v4i& a, const v4i& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a), __builtin_bit_cast(v8bf, b), c,
+                                                0, 0, 0);
+}
+
+struct StemArgs {
+  const uint16_t* xsp;   // [N][Hp][Wsp][8]
+  const uint16_t* wsp;   // [64][7][4][8]
+  uint16_t* y;           // [N][Ho][Wo][64]
+  float* part;           // [N*Ho][2][64] or null
+  uint32_t xsp_bytes;
+  int Hp, Wsp, Ho, Wo;
+  int rblocks;           // workgroups per image = ceil(Ho / ROWS)
+  int halo_rows;         // 2*ROWS + R - 2
+  int halo_alloc;        // bytes reserved for the halo (whole KiB)
+};
+
+}  // namespace
+
+template <int TM>
+__global__ void __launch_bounds__(STEM_ROWS * 64, 2) stem_conv_kernel(const StemArgs P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ws = smem;
+  char* Hs = smem + W_BYTES;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int n = blockIdx.x / P.rblocks;
+  const int ho0 = (blockIdx.x - n * P.rblocks) * STEM_ROWS;
+
+  // ---- stage: the input rows 2*ho0 .. 2*ho0 + halo_rows - 1 of image n (one contiguous span) by
+  // LDS-DMA, the packed weights by plain loads into the padded image
+  {
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.xsp, P.xsp_bytes);
+    const int rows = min(P.halo_rows, P.Hp - 2 * ho0);
+    const uint32_t span = (uint32_t)rows * P.Wsp * 16;
+    const uint32_t src0 = ((uint32_t)(n * P.Hp + 2 * ho0) * P.Wsp) * 16;
+    for (int q = wid; q * 1024 < P.halo_alloc; q += STEM_ROWS) {
+      const uint32_t o = (uint32_t)q * 1024 + lane * 16;
+      glds16(rx, Hs + q * 1024, o < span ? src0 + o : OOB);
+    }
+    const uint4* wg = reinterpret_cast<const uint4*>(P.wsp);
+    for (int i = t; i < STEM_K * 28; i += STEM_ROWS * 64) {
+      const int row = i / 28, c16 = i - row * 28;
+      *reinterpret_cast<uint4*>(Ws + row * W_PITCH + c16 * 16) = wg[i];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
+  __syncthreads();                                    // ... and every other wave's
+
+  const int ho = ho0 + wid;
+  if (ho >= P.Ho) return;  // past the image's last row (no barrier follows)
+  const int fr = lane & 15, fq = lane >> 4;
+
+  v4f acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const char* hrow = Hs + (2 * wid) * P.Wsp * 16 + (fr + fq) * 16;
+  const char* wrow = Ws + fr * W_PITCH + fq * 16;
+#pragma unroll
+  for (int r = 0; r < STEM_R; ++r) {
+    v4i a[4], b[TM];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const v4i*>(wrow + j * 16 * W_PITCH + r * STEM_SP * 16);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) b[i] = *reinterpret_cast<const v4i*>(hrow + (r * P.Wsp + i * 16) * 16);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[j], b[i], acc[i][j]);
+  }
+
+  // ---- epilogue: lane (fr, fq), register e of acc[i][j] = pixel i*16 + fr, channel j*16 + fq*4 + e
+  const int g = n * P.Ho + ho;  // BN partial group = this output row
+  if (P.part != nullptr) {
+    const float inv = 1.f / (float)P.Wo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s[4], q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) v += (i * 16 + fr < P.Wo) ? acc[i][j][e] : 0.f;
+        v = row_sum16(v);
+        const float mean = v * inv;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float d = acc[i][j][e] - mean;
+          m2 = (i * 16 + fr < P.Wo) ? fmaf(d, d, m2) : m2;
+        }
+        s[e] = v;
+        q[e] = row_sum16(m2);
+      }
+      if (fr == 0) {
+        float* pp = P.part + (int64_t)g * 2 * STEM_K + j * 16 + fq * 4;
+        *reinterpret_cast<float4*>(pp) = make_float4(s[0], s[1], s[2], s[3]);
+        *reinterpret_cast<float4*>(pp + STEM_K) = make_float4(q[0], q[1], q[2], q[3]);
+      }
+    }
+  }
+  uint16_t* yrow = P.y + (int64_t)g * P.Wo * STEM_K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int px = i * 16 + fr;
+    if (px < P.Wo) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 v;
+        v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+        v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(yrow + px * STEM_K + j * 16 + fq * 4) = v;
+      }
+    }
+  }
+}
+
+bool stem_halo_supported(int K, int R, int Sp, int Wo) {
+  return K == STEM_K && R == STEM_R && Sp == STEM_SP && Wo >= 1 && Wo <= 128;
+}
+
+void launch_stem_conv_fwd(const uint16_t* xsp, const uint16_t* wsp, uint16_t* y, float* part, int N, int Hp,
+                          int Wsp, int Ho, int Wo, hipStream_t st) {
+  if (Wo < 1 || Wo > 128 || Wsp != Wo + STEM_SP - 1 || 2 * (Ho - 1) + STEM_R > Hp)
+    throw std::runtime_error("stem_conv_fwd: unsupported geometry");
+  StemArgs a{};
+  a.xsp = xsp; a.wsp = wsp; a.y = y; a.part = part;
+  a.xsp_bytes = (uint32_t)((int64_t)N * Hp * Wsp * 16);
+  a.Hp = Hp; a.Wsp = Wsp; a.Ho = Ho; a.Wo = Wo;
+  a.rblocks = ceil_div(Ho, STEM_ROWS);
+  a.halo_rows = 2 * STEM_ROWS + STEM_R - 2;
+  const int tm = ceil_div(Wo, 16);
+  // every fragment read stays inside the allocation: last row + the widest tap past Wo
+  const int need = std::max(a.halo_rows * Wsp, (a.halo_rows - 1) * Wsp + tm * 16 + STEM_SP) * 16;
+  a.halo_alloc = ceil_div(need, 1024) * 1024;
+  const int smem = W_BYTES + a.halo_alloc;
+  dim3 grid(N * a.rblocks), blk(STEM_ROWS * 64);
+#define PDT_STEM(T)                                                                               \
+  case T: {                                                                                       \
+    static bool attr = false;                                                                     \
+    if (!attr) {                                                                                  \
+      hipFuncSetAttribute((const void*)stem_conv_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          160 * 1024);                                                            \
+      attr = true;                                                                                \
+    }                                                                                             \
+    hipLaunchKernelGGL(stem_conv_kernel<T>, grid, blk, smem, st, a);                              \
+    break;                                                                                        \
+  }
+  switch (tm) {
+    PDT_STEM(1) PDT_STEM(2) PDT_STEM(3) PDT_STEM(4) PDT_STEM(5) PDT_STEM(6) PDT_STEM(7) PDT_STEM(8)
+    default: throw std::runtime_error("stem_conv_fwd: Wo > 128");
+  }
+#undef PDT_STEM
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("stem_conv_fwd: ") + hipGetErrorString(e));
+}
+
+// ============================================================================
+//     Stem backward: BN-backward apply (through the max-pool gradient gather) fused into the
+//                    weight gradient -- the full-resolution stem gradient is never stored
+// ============================================================================
+// The stem's input gradient is not needed (the image takes no gradient), so dy = BN_bwd(maxpool_bwd
+// (dpool)) has exactly one consumer: the weight gradient.  Each workgroup loops over (image, output
+// row pair) items; per item it
+//   1. stages the 9 input super-pixel rows the pair reads (LDS-DMA, one contiguous span), and
+//   2. computes dy of the pair's 2*Wo pixels x 64 channels in registers -- pool quad gather
+//      (pool_quad.h), ReLU mask recomputed from y, BN-backward apply with the finished sums --
+//      straight into an LDS tile [pixel][channel] (128-B rows, swz128_tr layout),
+//   3. accumulates dW[64][224] += dy^T x im2col over the 2*Wo pixels on the MFMA: both operands
+//      have the pixel (reduction) index as their strided dimension, so fragments come from the
+//      CDNA4 transposing read ds_read_b64_tr_b16 -- on the halo the 32 (tap, channel) columns of
+//      a filter row are contiguous bytes starting at the pixel's super-pixel, rows overlapping.
+// Wave w owns dW column fragments {w, w+4, w+8, w+12} (< 14) for all four 16-row output-channel
+// fragments; the block's partial dW leaves once, at the end (fp32 atomics, or a private slab
+// reduced in fixed order for deterministic runs).  Replaces pool_bn_bwd_apply (writes dy, 411 MB
+// at batch 256) + the generic TN weight gradient (reads it back).
+namespace {
+
+constexpr int SB_THREADS = 256;
+constexpr int SB_COLS = STEM_R * STEM_SP * 8;  // 224 dW columns = (r, s, c)
+constexpr int SB_NJ = SB_COLS / 16;            // 14 column fragments
+
+struct StemBwdArgs {
+  const uint4* dp;       // pooled gradient [N][Hq][Wq][8] (8-channel vectors)
+  const uint2* idx;      // argmax bytes, same indexing
+  const uint4* y;        // stem conv output [N][Ho][Wo][8]
+  const float* stats;    // [4][64] mean, invstd, scale, shift
+  const float* gamma;    // [64]
+  const float* sums;     // [2][64] sum g, sum g*(y - mean)
+  float invM;
+  int train;
+  const uint16_t* xsp;
+  uint32_t xsp_bytes;
+  float* out;            // atomic: [64][224] (zeroed); slab: [gridDim.x][64*224]
+  int slab;
+  int Ho, Wo, Hq, Wq, Hp, Wsp;
+  int items;             // N * Ho / 2
+  int halo_alloc;
+};
+
+__device__ __forceinline__ int swz_tr128(int row, int chunk) {  // = conv_igemm.hip swz128_tr
+  const int sw = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return row * 128 + ((chunk ^ (sw << 1)) << 4);
+}
+
+typedef short v4s_tr __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4s_tr tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s_tr*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+__device__ __forceinline__ v4i tr_frag(const char* lo, const char* hi) {
+  return __builtin_bit_cast(v4i, __builtin_shufflevector(tr_read(lo), tr_read(hi), 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const StemBwdArgs P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  char* Ds = smem;                       // dy tile [2*Wo][64] bf16
+  char* Hs = smem + 2 * P.Wo * 128;      // 9 input rows
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.xsp, P.xsp_bytes);
+
+  // per-thread BN-backward coefficients of its fixed 8-channel group (256 % 8 == 0)
+  const int c8 = t & 7;
+  float k1[8], sgm[8], k2[8], mu[8], sc[8], sh[8];
+  {
+    float is[8], gm[8], s0[8], s1[8];
+    ld8f(P.stats + 64 + c8 * 8, is);
+    ld8f(P.gamma + c8 * 8, gm);
+    ld8f(P.stats + c8 * 8, mu);
+    ld8f(P.sums + c8 * 8, s0);
+    ld8f(P.sums + 64 + c8 * 8, s1);
+    ld8f(P.stats + 128 + c8 * 8, sc);
+    ld8f(P.stats + 192 + c8 * 8, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k1[j] = gm[j] * is[j];
+      sgm[j] = s0[j] * P.invM;
+      k2[j] = s1[j] * is[j] * is[j] * P.invM;
+    }
+  }
+
+  const int li = lane & 15, g = lane >> 4;
+  const int tq = li >> 2, tp = li & 3;
+  const bool j3 = wid + 12 < SB_NJ;  // waves 0, 1 own a fourth column fragment
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int hq2 = P.Ho >> 1;
+  const int npx = 2 * P.Wo;
+  for (int item = blockIdx.x; item < P.items; item += gridDim.x) {
+    const int n = item / hq2, a = item - n * hq2;
+    // 1. halo: input rows 4a .. 4a + 8 of image n
+    {
+      const int rows = min(9, P.Hp - 4 * a);
+      const uint32_t span = (uint32_t)rows * P.Wsp * 16;
+      const uint32_t src0 = ((uint32_t)(n * P.Hp + 4 * a) * P.Wsp) * 16;
+      for (int q = wid; q * 1024 < P.halo_alloc; q += SB_THREADS / 64) {
+        const uint32_t o = (uint32_t)q * 1024 + lane * 16;
+        glds16(rx, Hs + q * 1024, o < span ? src0 + o : OOB);
+      }
+    }
+    // 2. dy of the row pair (2a, 2a + 1): quad (a, b) x channel group c8 per unit
+    for (int u = t; u < P.Wq * 8; u += SB_THREADS) {
+      const int b = u >> 3;
+      const PoolQuad pq = pool_grad_quad(P.dp, P.idx, n, a, b, c8, 8, P.Hq, P.Wq);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int hh = e >> 1, w = 2 * b + (e & 1);
+        const f8 yy = unpack8(P.y[((int64_t)(n * P.Ho + 2 * a + hh) * P.Wo + w) * 8 + c8]);
+        f8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gr = fmaf(yy.v[j], sc[j], sh[j]) > 0.f ? pq.g[e].v[j] : 0.f;
+          o.v[j] = P.train ? k1[j] * (gr - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * gr;
+        }
+        *reinterpret_cast<uint4*>(Ds + swz_tr128(hh * P.Wo + w, c8)) = pack8(o);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // 3. dW += dy^T x im2col over the pair's pixels, 32 per K-step
+    for (int s = 0; s < npx / 32; ++s) {
+      const int p0 = s * 32 + 8 * g;           // this lane group's 8 pixels (one row: Wo % 16 == 0)
+      const int hh = p0 >= P.Wo ? 1 : 0;
+      const int wo0 = p0 - hh * P.Wo;
+      v4i af[4], bf[4];
+#pragma unroll
+      for (int im = 0; im < 4; ++im) {
+        const int ch = im * 2 + (tp >> 1), sub = (tp & 1) * 8;
+        af[im] = tr_frag(Ds + swz_tr128(p0 + tq, ch) + sub, Ds + swz_tr128(p0 + 4 + tq, ch) + sub);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int jn = jj < 3 || j3 ? wid + 4 * jj : wid;  // a 4th fragment only on waves 0, 1
+        const int r = jn >> 1, col0 = (jn & 1) * 16;
+        const char* base = Hs + ((2 * hh + r) * P.Wsp + wo0 + tq) * 16 + (col0 + 4 * tp) * 2;
+        bf[jj] = tr_frag(base, base + 4 * 16);
+      }
+#pragma unroll
+      for (int im = 0; im < 4; ++im)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[im][jj] = mfma16(af[im], bf[jj], acc[im][jj]);
+    }
+    __syncthreads();  // every wave done reading before the next item overwrites the tiles
+  }
+
+  // partial dW out: lane (fr = li, fq = g) of acc[im][jj] = row im*16 + g*4 + e, column jn*16 + li
+  float* o = P.slab ? P.out + (int64_t)blockIdx.x * 64 * SB_COLS : P.out;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    if (jj == 3 && !j3) break;
+    const int col = (wid + 4 * jj) * 16 + li;
+#pragma unroll
+    for (int im = 0; im < 4; ++im)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float* dst = o + (im * 16 + g * 4 + e) * SB_COLS + col;
+        if (P.slab) *dst = acc[im][jj][e];
+        else unsafeAtomicAdd(dst, acc[im][jj][e]);
+      }
+  }
+}
+
+__global__ void __launch_bounds__(256) stem_slab_reduce_kernel(const float* __restrict__ ws, int nslab,
+                                                               float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * SB_COLS) return;
+  float s = 0.f;
+  for (int b = 0; b < nslab; ++b) s += ws[(int64_t)b * 64 * SB_COLS + i];
+  out[i] = s;
+}
+
+bool stem_bwd_fused_supported(int K, int R, int Sp, int Ho, int Wo) {
+  return K == STEM_K && R == STEM_R && Sp == STEM_SP && Ho % 2 == 0 && Wo % 16 == 0 && Wo >= 16 && Wo <= 128;
+}
+
+int stem_bwd_fused_blocks(int N, int Ho) {
+  return std::max(1, std::min(N * Ho / 2, 512));
+}
+
+void launch_stem_bwd_fused(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y, const float* stats,
+                           const float* gamma, const float* sums, bool training, const uint16_t* xsp, int N,
+                           int Ho, int Wo, int Hp, int Wsp, float* dwsp, float* ws, hipStream_t st) {
+  if (!stem_bwd_fused_supported(STEM_K, STEM_R, STEM_SP, Ho, Wo) || Wsp != Wo + STEM_SP - 1 ||
+      2 * (Ho - 1) + STEM_R > Hp)
+    throw std::runtime_error("stem_bwd_fused: unsupported geometry");
+  StemBwdArgs a{};
+  a.dp = reinterpret_cast<const uint4*>(dpool);
+  a.idx = reinterpret_cast<const uint2*>(idx);
+  a.y = reinterpret_cast<const uint4*>(y);
+  a.stats = stats; a.gamma = gamma; a.sums = sums;
+  a.invM = 1.f / (float)((int64_t)N * Ho * Wo);
+  a.train = training ? 1 : 0;
+  a.xsp = xsp;
+  a.xsp_bytes = (uint32_t)((int64_t)N * Hp * Wsp * 16);
+  a.Ho = Ho; a.Wo = Wo; a.Hq = Ho / 2; a.Wq = Wo / 2; a.Hp = Hp; a.Wsp = Wsp;
+  a.items = N * Ho / 2;
+  a.halo_alloc = ceil_div(9 * Wsp * 16, 1024) * 1024;
+  const int grid = stem_bwd_fused_blocks(N, Ho);
+  a.slab = ws != nullptr ? 1 : 0;
+  a.out = ws != nullptr ? ws : dwsp;
+  if (!a.slab) hipMemsetAsync(dwsp, 0, 64 * SB_COLS * sizeof(float), st);
+  const int smem = 2 * Wo * 128 + a.halo_alloc;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)stem_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(stem_bwd_fused_kernel, dim3(grid), dim3(SB_THREADS), smem, st, a);
+  if (a.slab)
+    hipLaunchKernelGGL(stem_slab_reduce_kernel, dim3(ceil_div(64 * SB_COLS, 256)), dim3(256), 0, st, ws, grid,
+                       dwsp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("stem_bwd_fused: ") + hipGetErrorString(e));
+}
+
+}  // namespace pdt

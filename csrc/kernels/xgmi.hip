@@ -55,13 +55,18 @@ __global__ void xgmi_signal_kernel(XgmiPtrs P, int world, int rank, int slot, un
 __global__ void xgmi_wait_kernel(const unsigned* flags, int world, int slot, unsigned epoch,
                                  unsigned long long timeout_ticks, unsigned* err, unsigned code) {
   const int q = threadIdx.x;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // already failed
   const unsigned long long t0 = wall_clock64();
   bool done = q >= world;
   while (true) {
     if (!done) done = (int)(ld_acquire_sys(flags + slot * kXgmiMaxRanks + q) - epoch) >= 0;
     if (__all(done)) break;
     if (wall_clock64() - t0 > timeout_ticks) {
-      if (q == 0) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (q == 0) {  // keep the FIRST failure's code
+        unsigned expected = 0u;
+        __hip_atomic_compare_exchange_strong(err, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       break;
     }
     __builtin_amdgcn_s_sleep(2);

@@ -261,7 +261,7 @@ class _StemConvBN(torch.autograd.Function):
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, pad, training,
                 momentum, eps):
         C = native()
-        xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
+        xsp, y, part, grows = C.stem_conv_fwd(x, weight, stride, pad, training)
         k = weight.shape[0]
         count = y.shape[0] * y.shape[1] * y.shape[2]
         buffers_ready()
@@ -270,7 +270,7 @@ class _StemConvBN(torch.autograd.Function):
                 running_mean = torch.zeros(k, device=x.device)
                 running_var = torch.ones(k, device=x.device)
             stats = C.bn_finalize(part, count, running_mean, running_var, gamma, beta,
-                                  float(momentum), float(eps))
+                                  float(momentum), float(eps), grows)
         else:
             stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
         z = C.bn_act_fwd(y, stats[2], stats[3], None, True)
@@ -316,7 +316,7 @@ class _StemConvBNPool(torch.autograd.Function):
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, pad, training,
                 momentum, eps):
         C = native()
-        xsp, y, part = C.stem_conv_fwd(x, weight, stride, pad, training)
+        xsp, y, part, grows = C.stem_conv_fwd(x, weight, stride, pad, training)
         k = weight.shape[0]
         count = y.shape[0] * y.shape[1] * y.shape[2]
         buffers_ready()
@@ -325,7 +325,7 @@ class _StemConvBNPool(torch.autograd.Function):
                 running_mean = torch.zeros(k, device=x.device)
                 running_var = torch.ones(k, device=x.device)
             stats = C.bn_finalize(part, count, running_mean, running_var, gamma, beta,
-                                  float(momentum), float(eps))
+                                  float(momentum), float(eps), grows)
         else:
             stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
         out, idx = C.bn_relu_maxpool(y, stats[2], stats[3])
@@ -353,8 +353,24 @@ class _StemConvBNPool(torch.autograd.Function):
         else:
             sums = C.pool_bn_bwd_reduce(dout, idx, y, stats)
             dgamma, dbeta = (sums[1] * stats[1]).to(gamma.dtype), sums[0].to(gamma.dtype)
-        dy = C.pool_bn_bwd_apply(dout, idx, y, stats, gamma, sums, ctx.training)
         dw = None
+        if ctx.needs_input_grad[1] and _STEM_BWD_FUSED and C.stem_bwd_fused_supported(
+                weight.shape[0], weight.shape[2], (weight.shape[3] + 2) // 2, y.shape[1], y.shape[2]):
+            # the image takes no gradient, so dy's only consumer is the weight gradient: the BN/pool
+            # backward apply runs inside it and the full-resolution dy is never stored
+            sink = _grad_sink(weight)
+            if sink is not None:
+                C.stem_bwd_fused(dout, idx, y, stats, gamma, sums, ctx.training, xsp, list(weight.shape),
+                                 deterministic(), sink)
+                sunk.append(weight)
+            else:
+                dw = C.stem_bwd_fused(dout, idx, y, stats, gamma, sums, ctx.training, xsp, list(weight.shape),
+                                      deterministic()).to(weight.dtype)
+            if sunk:
+                sunk[0]._pdt_flat.mark_ready(sunk)
+            ctx.weight = None
+            return (None, dw, dgamma, dbeta, None, None, None, None, None, None, None)
+        dy = C.pool_bn_bwd_apply(dout, idx, y, stats, gamma, sums, ctx.training)
         if ctx.needs_input_grad[1]:
             sink = _grad_sink(weight)
             if sink is not None:
@@ -369,6 +385,7 @@ class _StemConvBNPool(torch.autograd.Function):
 
 
 _STEM_POOL = os.environ.get("PDT_STEM_POOL", "1") != "0"  # debugging switch (default on)
+_STEM_BWD_FUSED = os.environ.get("PDT_STEM_BWD_FUSED", "1") != "0"  # A/B switch (default on)
 
 
 def _stem_fast(x: torch.Tensor, conv: nn.Conv2d) -> bool:
