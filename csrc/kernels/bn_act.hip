@@ -391,6 +391,27 @@ __device__ __forceinline__ float relu_grad(float g, float zv, float yv, float sc
   return g;
 }
 
+// Tree sum over the `rpi` threads that share a channel group (thread t = roff * step + c): 16
+// values per thread in a value-major LDS image sh[j * 256 + t]; the totals end in the roff == 0
+// threads' slots.  256 threads per block.
+__device__ __forceinline__ void block_tree_sum16(float* sh, int t, int rpi, int step, const float (&a)[8],
+                                                 const float (&b)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[j * 256 + t] = a[j];
+    sh[(8 + j) * 256 + t] = b[j];
+  }
+  __syncthreads();
+  const int roff = t / step;
+  for (int s = rpi / 2; s > 0; s >>= 1) {
+    if (roff < s) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sh[j * 256 + t] += sh[j * 256 + t + s * step];
+    }
+    __syncthreads();
+  }
+}
+
 // stats = [4][K]: mean, invstd, scale, shift (bn_finalize output)
 template <int MASK>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restrict__ dz,
@@ -428,23 +449,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_stage1(const uint4* __restr
       sgx[j] = fmaf(g, yy.v[j] - mu[j], sgx[j]);
     }
   }
-  // block reduction over threads with equal c8: sh[roff][c8*16 + j]
-  float* my = sh + (size_t)t * 16;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { my[j] = sg[j]; my[8 + j] = sgx[j]; }
-  __syncthreads();
-  for (int s = rpi / 2; s > 0; s >>= 1) {
-    if (roff < s) {
-      float* o = sh + (size_t)(t + s * CH8) * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) my[j] += o[j];
-    }
-    __syncthreads();
-  }
+  // block reduction over threads with equal c8, in a value-major LDS image sh[j][thread]:
+  // consecutive lanes hit consecutive banks (the thread-major [thread][16] image cost ~16
+  // conflict cycles per LDS instruction, profiles/r2s2_sq_mfma_busy_per_kernel.txt)
+  block_tree_sum16(sh, t, rpi, CH8, sg, sgx);
   if (roff == 0) {
     float* o = ws + (int64_t)blockIdx.x * 2 * K;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = my[j]; o[K + c8 * 8 + j] = my[8 + j]; }
+    for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = sh[j * 256 + t]; o[K + c8 * 8 + j] = sh[(8 + j) * 256 + t]; }
   }
 }
 
@@ -792,12 +804,20 @@ __global__ void __launch_bounds__(256) pool_bn_bwd_reduce_kernel(const uint4* __
   for (int qd = q0 + roff; qd < q1; qd += rpi) {
     int n, a, b;
     quad_coords((uint32_t)qd, Ho, Wo, n, a, b);
+    // the quad's 4 y vectors are issued first: they do not depend on the argmax gather below (an
+    // odd-edge pixel reads its clamped neighbour and is skipped)
+    uint4 yv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int h = min(2 * a + (e >> 1), H - 1), w = min(2 * b + (e & 1), W - 1);
+      yv[e] = y[(((int64_t)n * H + h) * W + w) * K8 + c8];
+    }
     const PoolQuad pq = pool_grad_quad(dp, idx, n, a, b, c8, K8, Ho, Wo);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int h = 2 * a + (e >> 1), w = 2 * b + (e & 1);
       if (h >= H || w >= W) continue;
-      const f8 yy = unpack8(y[(((int64_t)n * H + h) * W + w) * K8 + c8]);
+      const f8 yy = unpack8(yv[e]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float g = relu_grad<2>(pq.g[e].v[j], 0.f, yy.v[j], sc[j], shf[j]);
@@ -806,22 +826,11 @@ __global__ void __launch_bounds__(256) pool_bn_bwd_reduce_kernel(const uint4* __
       }
     }
   }
-  float* my = sh + (size_t)t * 16;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { my[j] = sg[j]; my[8 + j] = sgx[j]; }
-  __syncthreads();
-  for (int s = rpi / 2; s > 0; s >>= 1) {
-    if (roff < s) {
-      const float* o = sh + (size_t)(t + s * K8) * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) my[j] += o[j];
-    }
-    __syncthreads();
-  }
+  block_tree_sum16(sh, t, rpi, K8, sg, sgx);  // value-major LDS image: conflict-free
   if (roff == 0) {
     float* o = ws + (int64_t)blockIdx.x * 2 * K;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = my[j]; o[K + c8 * 8 + j] = my[8 + j]; }
+    for (int j = 0; j < 8; ++j) { o[c8 * 8 + j] = sh[j * 256 + t]; o[K + c8 * 8 + j] = sh[(8 + j) * 256 + t]; }
   }
 }
 

@@ -60,112 +60,166 @@ struct StemArgs {
   float* part;           // [N*Ho][2][64] or null
   uint32_t xsp_bytes;
   int Hp, Wsp, Ho, Wo;
-  int rblocks;           // workgroups per image = ceil(Ho / ROWS)
+  int nimg;              // images
+  int rblocks;           // row groups per image = ceil(Ho / ROWS)
   int halo_rows;         // 2*ROWS + R - 2
   int halo_alloc;        // bytes reserved for the halo (whole KiB)
 };
 
 }  // namespace
 
-template <int TM>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS barrier without the compiler's memory-model drain: ds traffic is waited for, VMEM (the
+// previous group's output stores, the next halo's DMA) stays in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void buf_store16(const uint4& v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, r, (int)off, 0, 0);
+}
+
+// Persistent: the grid is sized to the resident capacity (2 workgroups per CU) and each workgroup
+// walks row groups g = blockIdx.x, +gridDim.x, ...; the packed weights are staged once, and the
+// halo of the NEXT row group is fetched by LDS-DMA into the second halo buffer while this one
+// computes.  Per group every wave issues exactly N_AFTER vector-memory ops after that DMA (its BN
+// partial and output stores: buffer stores whose masked lanes get an out-of-range offset, so the
+// instruction count never depends on the data or the shape), so the halo wait one group later is
+// vmcnt(N_AFTER) -- the output stores keep draining underneath the next group's MFMA.
+//
+// Output: after the MFMA loop (and a barrier) the finished halo buffer is reused as a per-wave
+// [16 px][128 B] staging tile (16-byte chunks XOR-swizzled by pixel), so every output store
+// instruction writes 1 KB of contiguous y (8 whole pixels).  Stored straight from the MFMA layout
+// the same bytes leave as 16 x 32-byte fragments per instruction and run at ~40% of the rate
+// (scripts/bench_stem.py: 2.4 vs 5.9 TB/s for the output alone).
+template <int TM, bool STATS>
 __global__ void __launch_bounds__(STEM_ROWS * 64, 2) stem_conv_kernel(const StemArgs P) {
+  constexpr int N_AFTER = 2 * TM + (STATS ? 8 : 0);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ws = smem;
-  char* Hs = smem + W_BYTES;
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int n = blockIdx.x / P.rblocks;
-  const int ho0 = (blockIdx.x - n * P.rblocks) * STEM_ROWS;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.xsp, P.xsp_bytes);
+  const int ngroups = P.nimg * P.rblocks;
 
-  // ---- stage: the input rows 2*ho0 .. 2*ho0 + halo_rows - 1 of image n (one contiguous span) by
-  // LDS-DMA, the packed weights by plain loads into the padded image
-  {
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.xsp, P.xsp_bytes);
+  // input rows 2*ho0 .. 2*ho0 + halo_rows - 1 of the group's image: one contiguous span
+  auto issue_halo = [&](int grp, char* dst) {
+    const int n = grp / P.rblocks;
+    const int ho0 = (grp - n * P.rblocks) * STEM_ROWS;
     const int rows = min(P.halo_rows, P.Hp - 2 * ho0);
     const uint32_t span = (uint32_t)rows * P.Wsp * 16;
     const uint32_t src0 = ((uint32_t)(n * P.Hp + 2 * ho0) * P.Wsp) * 16;
     for (int q = wid; q * 1024 < P.halo_alloc; q += STEM_ROWS) {
       const uint32_t o = (uint32_t)q * 1024 + lane * 16;
-      glds16(rx, Hs + q * 1024, o < span ? src0 + o : OOB);
+      glds16(rx, dst + q * 1024, o < span ? src0 + o : OOB);
     }
+  };
+
+  int grp = blockIdx.x;
+  if (grp < ngroups) issue_halo(grp, smem + W_BYTES);
+  {  // packed weights, once per workgroup
     const uint4* wg = reinterpret_cast<const uint4*>(P.wsp);
     for (int i = t; i < STEM_K * 28; i += STEM_ROWS * 64) {
       const int row = i / 28, c16 = i - row * 28;
       *reinterpret_cast<uint4*>(Ws + row * W_PITCH + c16 * 16) = wg[i];
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
-  __syncthreads();                                    // ... and every other wave's
-
-  const int ho = ho0 + wid;
-  if (ho >= P.Ho) return;  // past the image's last row (no barrier follows)
   const int fr = lane & 15, fq = lane >> 4;
-
-  v4f acc[TM][4];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  const char* hrow = Hs + (2 * wid) * P.Wsp * 16 + (fr + fq) * 16;
   const char* wrow = Ws + fr * W_PITCH + fq * 16;
-#pragma unroll
-  for (int r = 0; r < STEM_R; ++r) {
-    v4i a[4], b[TM];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const v4i*>(wrow + j * 16 * W_PITCH + r * STEM_SP * 16);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) b[i] = *reinterpret_cast<const v4i*>(hrow + (r * P.Wsp + i * 16) * 16);
+  const bool lastok = (TM - 1) * 16 + fr < P.Wo;  // the last pixel fragment may be partial
+  for (int it = 0; grp < ngroups; grp += gridDim.x, ++it) {
+    char* Hs = smem + W_BYTES + (it & 1) * P.halo_alloc;
+    if (it == 0) wait_vm<0>();
+    else wait_vm<N_AFTER>();  // this group's halo landed (the last group's stores may not have)
+    lds_barrier();            // ... for every wave; and every wave is done with the other buffer
+    const int nxt = grp + gridDim.x;
+    if (nxt < ngroups) issue_halo(nxt, smem + W_BYTES + ((it + 1) & 1) * P.halo_alloc);
+
+    const int n = grp / P.rblocks;
+    const int ho = (grp - n * P.rblocks) * STEM_ROWS + wid;
+    const bool valid = ho < P.Ho;  // a wave past the image's last row stores nothing (all offsets OOB)
+    const int g = n * P.Ho + min(ho, P.Ho - 1);  // BN partial group = this output row
+
+    v4f acc[TM][4];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[j], b[i], acc[i][j]);
-  }
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    const char* hrow = Hs + (2 * wid) * P.Wsp * 16 + (fr + fq) * 16;
+#pragma unroll
+    for (int r = 0; r < STEM_R; ++r) {
+      v4i a[4], b[TM];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const v4i*>(wrow + j * 16 * W_PITCH + r * STEM_SP * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) b[i] = *reinterpret_cast<const v4i*>(hrow + (r * P.Wsp + i * 16) * 16);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[j], b[i], acc[i][j]);
+    }
 
-  // ---- epilogue: lane (fr, fq), register e of acc[i][j] = pixel i*16 + fr, channel j*16 + fq*4 + e
-  const int g = n * P.Ho + ho;  // BN partial group = this output row
-  if (P.part != nullptr) {
-    const float inv = 1.f / (float)P.Wo;
+    // ---- BN partials: lane (fr, fq), register e of acc[i][j] = pixel i*16 + fr, channel
+    // j*16 + fq*4 + e; per channel the row's sum and M2 about the row mean (two passes)
+    if constexpr (STATS) {
+      const __amdgpu_buffer_rsrc_t rp = make_rsrc(P.part + (int64_t)g * 2 * STEM_K, valid ? 2 * STEM_K * 4 : 0);
+      const float inv = 1.f / (float)P.Wo;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float s[4], q[4];
+      for (int j = 0; j < 4; ++j) {
+        float sm[4], q[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = 0.f;
+        for (int e = 0; e < 4; ++e) {
+          float v = 0.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) v += (i * 16 + fr < P.Wo) ? acc[i][j][e] : 0.f;
-        v = row_sum16(v);
-        const float mean = v * inv;
-        float m2 = 0.f;
+          for (int i = 0; i < TM; ++i) v += (i < TM - 1 || lastok) ? acc[i][j][e] : 0.f;
+          v = row_sum16(v);
+          const float mean = v * inv;
+          float m2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const float d = acc[i][j][e] - mean;
-          m2 = (i * 16 + fr < P.Wo) ? fmaf(d, d, m2) : m2;
+          for (int i = 0; i < TM; ++i) {
+            const float d = acc[i][j][e] - mean;
+            m2 = (i < TM - 1 || lastok) ? fmaf(d, d, m2) : m2;
+          }
+          sm[e] = v;
+          q[e] = row_sum16(m2);
         }
-        s[e] = v;
-        q[e] = row_sum16(m2);
-      }
-      if (fr == 0) {
-        float* pp = P.part + (int64_t)g * 2 * STEM_K + j * 16 + fq * 4;
-        *reinterpret_cast<float4*>(pp) = make_float4(s[0], s[1], s[2], s[3]);
-        *reinterpret_cast<float4*>(pp + STEM_K) = make_float4(q[0], q[1], q[2], q[3]);
+        const uint32_t off = (uint32_t)(j * 16 + fq * 4) * 4;
+        buf_store16(make_uint4(__float_as_uint(sm[0]), __float_as_uint(sm[1]), __float_as_uint(sm[2]),
+                               __float_as_uint(sm[3])), rp, fr == 0 ? off : OOB);
+        buf_store16(make_uint4(__float_as_uint(q[0]), __float_as_uint(q[1]), __float_as_uint(q[2]),
+                               __float_as_uint(q[3])), rp, fr == 0 ? off + STEM_K * 4 : OOB);
       }
     }
-  }
-  uint16_t* yrow = P.y + (int64_t)g * P.Wo * STEM_K;
+
+    // ---- output through the staging tile
+    lds_barrier();  // every wave is done reading this halo buffer
+    char* stg = Hs + wid * 2048;
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(P.y + (int64_t)g * P.Wo * STEM_K, valid ? P.Wo * STEM_K * 2 : 0);
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int px = i * 16 + fr;
-    if (px < P.Wo) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         uint2 v;
         v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-        *reinterpret_cast<uint2*>(yrow + px * STEM_K + j * 16 + fq * 4) = v;
+        const int c = 2 * j + (fq >> 1);
+        *reinterpret_cast<uint2*>(stg + fr * 128 + ((c ^ (fr & 7)) * 16) + (fq & 1) * 8) = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pp = k * 8 + (lane >> 3), c = lane & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(stg + pp * 128 + ((c ^ (pp & 7)) * 16));
+        const int px = i * 16 + pp;
+        buf_store16(v, ry, px < P.Wo ? (uint32_t)(px * STEM_K + c * 8) * 2 : OOB);
       }
     }
   }
+  wait_vm<0>();
 }
 
 bool stem_halo_supported(int K, int R, int Sp, int Wo) {
@@ -180,30 +234,40 @@ void launch_stem_conv_fwd(const uint16_t* xsp, const uint16_t* wsp, uint16_t* y,
   a.xsp = xsp; a.wsp = wsp; a.y = y; a.part = part;
   a.xsp_bytes = (uint32_t)((int64_t)N * Hp * Wsp * 16);
   a.Hp = Hp; a.Wsp = Wsp; a.Ho = Ho; a.Wo = Wo;
+  a.nimg = N;
   a.rblocks = ceil_div(Ho, STEM_ROWS);
   a.halo_rows = 2 * STEM_ROWS + STEM_R - 2;
   const int tm = ceil_div(Wo, 16);
   // every fragment read stays inside the allocation: last row + the widest tap past Wo
   const int need = std::max(a.halo_rows * Wsp, (a.halo_rows - 1) * Wsp + tm * 16 + STEM_SP) * 16;
-  a.halo_alloc = ceil_div(need, 1024) * 1024;
-  const int smem = W_BYTES + a.halo_alloc;
-  dim3 grid(N * a.rblocks), blk(STEM_ROWS * 64);
-#define PDT_STEM(T)                                                                               \
-  case T: {                                                                                       \
+  // (at least the ROWS x 2 KB output staging tiles that reuse a finished halo buffer)
+  a.halo_alloc = std::max(ceil_div(need, 1024) * 1024, STEM_ROWS * 2048);
+  const int smem = W_BYTES + 2 * a.halo_alloc;  // weights + double-buffered halo
+  int dev = 0, cus = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int resident = 2 * std::max(cus, 1);  // 2 workgroups per CU (LDS: 2 x 78 KB at 224 px)
+  dim3 grid(std::max(1, std::min(N * a.rblocks, resident))), blk(STEM_ROWS * 64);
+#define PDT_STEM_S(T, S)                                                                          \
+  {                                                                                               \
     static bool attr = false;                                                                     \
     if (!attr) {                                                                                  \
-      hipFuncSetAttribute((const void*)stem_conv_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+      hipFuncSetAttribute((const void*)stem_conv_kernel<T, S>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                           160 * 1024);                                                            \
       attr = true;                                                                                \
     }                                                                                             \
-    hipLaunchKernelGGL(stem_conv_kernel<T>, grid, blk, smem, st, a);                              \
-    break;                                                                                        \
+    hipLaunchKernelGGL((stem_conv_kernel<T, S>), grid, blk, smem, st, a);                         \
   }
+#define PDT_STEM(T)                                                                               \
+  case T:                                                                                         \
+    if (part != nullptr) PDT_STEM_S(T, true) else PDT_STEM_S(T, false)                            \
+    break;
   switch (tm) {
     PDT_STEM(1) PDT_STEM(2) PDT_STEM(3) PDT_STEM(4) PDT_STEM(5) PDT_STEM(6) PDT_STEM(7) PDT_STEM(8)
     default: throw std::runtime_error("stem_conv_fwd: Wo > 128");
   }
 #undef PDT_STEM
+#undef PDT_STEM_S
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("stem_conv_fwd: ") + hipGetErrorString(e));
 }
@@ -328,11 +392,15 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
     // 2. dy of the row pair (2a, 2a + 1): quad (a, b) x channel group c8 per unit
     for (int u = t; u < P.Wq * 8; u += SB_THREADS) {
       const int b = u >> 3;
+      uint4 yv[4];  // issued before the argmax gather: independent of it (one round trip, not two)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        yv[e] = P.y[((int64_t)(n * P.Ho + 2 * a + (e >> 1)) * P.Wo + 2 * b + (e & 1)) * 8 + c8];
       const PoolQuad pq = pool_grad_quad(P.dp, P.idx, n, a, b, c8, 8, P.Hq, P.Wq);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int hh = e >> 1, w = 2 * b + (e & 1);
-        const f8 yy = unpack8(P.y[((int64_t)(n * P.Ho + 2 * a + hh) * P.Wo + w) * 8 + c8]);
+        const f8 yy = unpack8(yv[e]);
         f8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -400,7 +468,7 @@ bool stem_bwd_fused_supported(int K, int R, int Sp, int Ho, int Wo) {
   return K == STEM_K && R == STEM_R && Sp == STEM_SP && Ho % 2 == 0 && Wo % 16 == 0 && Wo >= 16 && Wo <= 128;
 }
 
-int stem_bwd_fused_blocks(int N, int Ho) {
+int stem_bwd_fused_blocks(int N, int Ho) {  // 3 resident blocks per CU (45 KB LDS each)
   return std::max(1, std::min(N * Ho / 2, 512));
 }
 
