@@ -121,6 +121,9 @@ def main(argv=None) -> int:
     dev_index = 0 if args.share_device else env.local_rank
     if torch.cuda.is_available():
         torch.cuda.set_device(dev_index)
+        if args.impl == "native":
+            from pytorch_distributed_tutorials_amd.ops.streams import use_critical_stream
+            use_critical_stream(torch.device("cuda", dev_index))
     dev = torch.device(f"cuda:{dev_index}" if torch.cuda.is_available() else "cpu")
     dev_ids = [dev_index] if dev.type == "cuda" else None
     torch.manual_seed(0)

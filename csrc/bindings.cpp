@@ -1271,6 +1271,25 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_counter_bank", [](uintptr_t stream) {
     return pdt::bn_counter_bank(reinterpret_cast<hipStream_t>(stream));
   }, py::arg("stream"));
+  // Stream restricted to `ncu` of the device's CUs, evenly spaced over the CU index space (side
+  // streams that should leave the rest of the chip to the critical path).  Returns the raw
+  // hipStream_t (wrap with torch.cuda.ExternalStream); it lives until the process exits.
+  m.def("cu_masked_stream", [](int device, int ncu) {
+    c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+    int total = 0;
+    if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || total <= 0)
+      throw std::runtime_error("cu_masked_stream: cannot query the CU count");
+    ncu = std::max(1, std::min(ncu, total));
+    std::vector<uint32_t> mask((total + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) {
+      const int cu = (int)((int64_t)i * total / ncu);
+      mask[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t s = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+    return reinterpret_cast<uintptr_t>(s);
+  }, py::arg("device"), py::arg("ncu"));
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check_enabled", []() { return g_sync_check; });
 

@@ -203,6 +203,10 @@ def main(argv: Optional[list] = None) -> int:
         ops.set_fp8(True)
     if args.graph and (impl != "native" or device.type != "cuda"):
         raise SystemExit("--graph needs the native impl on a GPU")
+    if impl == "native" and device.type == "cuda":
+        torch.cuda.set_device(device)
+        from .ops.streams import use_critical_stream
+        use_critical_stream(device)  # the step's critical path outranks the side streams
     autocast = (impl == "torch" and dtype == "bf16")
     if args.trace:
         trace.enable(True)
