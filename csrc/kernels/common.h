@@ -25,8 +25,13 @@ __device__ __forceinline__ bf16 f2bf(float f) {
   return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
+// Two floats -> two RNE bf16 in one dword: ONE v_cvt_pk_bf16_f32 (the scalar-conversion form
+// above, or-ed together, compiles to two conversions + shift + or where the pair is not
+// recognised -- 4 VALU per pair in the conv epilogues).
+typedef float pdt_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pdt_bf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(pdt_f2{lo, hi}, pdt_bf2));
 }
 
 // 16-byte vector of 8 bf16 <-> 8 floats

@@ -744,47 +744,69 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   constexpr int IT_MAX = PDT_EPI_IT;  // (y, z, addend) chunks in flight per lane and batch
   constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
   static_assert(IT_ALL % IT == 0, "chunk batches");
-  // The BN mask mode and the addend are wave-uniform: dispatch ONCE to a copy of the batch loop
-  // specialised on both (per-element tests of kernel arguments cost ~6x the SALU and 2.5x the
-  // VALU instructions of the plain epilogue, measured).
-  auto run_batches = [&](auto mm_c, auto ha_c) {
+  // The BN mask mode, the addend and the output addressing are wave-uniform: dispatch ONCE to a
+  // copy of the batch loop specialised on them (per-element tests of kernel arguments cost ~6x
+  // the SALU and 2.5x the VALU instructions of the plain epilogue, measured).
+  //   DN: dense output (GEMM row == NHWC pixel) and, if any, an addend at the same offsets -- a
+  //       chunk's offset is then the lane's base + a compile-time multiple of the row pitch (one
+  //       add and one compare per chunk instead of the pixel decomposition's ~12 VALU).
+  // Mask mode 3 (bitmask) masks the PACKED bf16 chunk: per pair of channels two sign-extended
+  // bit fields merged by one v_bfi_b32 give the 32-bit keep-mask, so g is never unpacked, masked
+  // and re-packed (the chunk was rounded to bf16 already: same bits as masking in fp32).
+  auto run_batches = [&](auto mm_c, auto ha_c, auto dn_c) {
     constexpr int MM = decltype(mm_c)::value;   // 0 none, 1 z > 0, 2 y*sc+sh > 0, 3 bitmask
     constexpr bool HA = decltype(ha_c)::value;  // residual-gradient addend
+    constexpr bool DN = decltype(dn_c)::value;  // dense addressing fast path
+    constexpr int RSTEP = 64 / CH_PER_ROW;      // staging rows advanced per chunk slot
+    const int c_l = lane % CH_PER_ROW, r_l = lane / CH_PER_ROW;
+    const int col_l = wcol0 + c_l * 8;
+    const int mrem = (col_l < P.Nout) ? P.M - (wrow0 + r_l) : 0;  // rows this lane may still touch
+    const uint32_t off_l = ((uint32_t)(wrow0 + r_l) * (uint32_t)P.Nout + (uint32_t)col_l) * 2u;
+    const uint32_t pitch = (uint32_t)P.Nout * 2u * RSTEP;  // bytes between a lane's chunks
 #pragma unroll 1
     for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
       uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
       uint32_t aoff[IT];  // byte offset of the chunk in a compact (stride-2) addend, or OOB
+      if constexpr (DN) {
+        const uint32_t ob = off_l + (uint32_t)b0 * pitch;
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int qd = lane + (b0 + it) * 64;
-        const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-        const int m = wrow0 + r;
-        const int col = wcol0 + c * 8;
-        ooff[it] = OOB;
-        aoff[it] = OOB;
-        if (m < P.M && col < P.Nout) {
-          // 32-bit offsets: every operand is addressed through a buffer resource (< 4 GiB)
-          uint32_t orow = (uint32_t)m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel
-          if (!P.dense || (HA && P.add_sub)) {
-            uint32_t n = fdiv((uint32_t)m, P.div_ij);
-            uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
-            uint32_t ii = fdiv(rem, P.div_j);
-            uint32_t jj = rem - ii * (uint32_t)P.Mj;
-            if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
-              orow = (n * (uint32_t)P.OH + ii * (uint32_t)P.osh + (uint32_t)P.oph) * (uint32_t)P.OW +
-                     jj * (uint32_t)P.osw + (uint32_t)P.opw;
-            if (HA && P.add_sub) {
-              // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
-              // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
-              const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
-              const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
-              if (((hh | ww) & 1) == 0)
-                aoff[it] = (((n * (uint32_t)P.add_h + (uint32_t)(hh >> 1)) * (uint32_t)P.add_w + (uint32_t)(ww >> 1)) *
-                                (uint32_t)P.Nout + (uint32_t)col) * 2u;
+        for (int it = 0; it < IT; ++it) {
+          ooff[it] = (b0 + it) * RSTEP < mrem ? ob + (uint32_t)it * pitch : OOB;
+          aoff[it] = ooff[it];
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          const int qd = lane + (b0 + it) * 64;
+          const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+          const int m = wrow0 + r;
+          const int col = wcol0 + c * 8;
+          ooff[it] = OOB;
+          aoff[it] = OOB;
+          if (m < P.M && col < P.Nout) {
+            // 32-bit offsets: every operand is addressed through a buffer resource (< 4 GiB)
+            uint32_t orow = (uint32_t)m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel
+            if (!P.dense || (HA && P.add_sub)) {
+              uint32_t n = fdiv((uint32_t)m, P.div_ij);
+              uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+              uint32_t ii = fdiv(rem, P.div_j);
+              uint32_t jj = rem - ii * (uint32_t)P.Mj;
+              if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+                orow = (n * (uint32_t)P.OH + ii * (uint32_t)P.osh + (uint32_t)P.oph) * (uint32_t)P.OW +
+                       jj * (uint32_t)P.osw + (uint32_t)P.opw;
+              if (HA && P.add_sub) {
+                // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
+                // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
+                const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
+                const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
+                if (((hh | ww) & 1) == 0)
+                  aoff[it] = (((n * (uint32_t)P.add_h + (uint32_t)(hh >> 1)) * (uint32_t)P.add_w + (uint32_t)(ww >> 1)) *
+                                  (uint32_t)P.Nout + (uint32_t)col) * 2u;
+              }
             }
+            ooff[it] = (orow * (uint32_t)P.Nout + (uint32_t)col) * 2u;
+            if (HA && !P.add_sub) aoff[it] = ooff[it];
           }
-          ooff[it] = (orow * (uint32_t)P.Nout + (uint32_t)col) * 2u;
-          if (HA && !P.add_sub) aoff[it] = ooff[it];
         }
       }
       v4i av[IT], yv[IT], zv[IT];
@@ -824,24 +846,35 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
           // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
           // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
           // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
+          if constexpr (MM == 3) {
+            const int zb = zv[it][0];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h, 1);      // 0 or ~0
+              const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h + 1, 1);
+              const uint32_t keep = (0x0000ffffu & lo) | (~0x0000ffffu & hi);         // v_bfi_b32
+              v[h] = (int)((uint32_t)v[h] & keep);
+            }
+          }
           f8 a = unpack8(__builtin_bit_cast(uint4, v));
           const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
-          f8 zz;
-          if constexpr (MM == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
-          uint32_t zbits = 0u;
-          if constexpr (MM == 3) zbits = (uint32_t)zv[it][0];
+          if constexpr (MM == 1 || MM == 2) {
+            f8 zz;
+            if constexpr (MM == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              bool on;
+              if constexpr (MM == 1) on = zz.v[q] > 0.f;
+              else on = fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f;
+              a.v[q] = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
+            }
+            v = __builtin_bit_cast(v4i, pack8(a));
+          }
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            bool on = true;
-            if constexpr (MM == 1) on = zz.v[q] > 0.f;
-            if constexpr (MM == 2) on = fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f;
-            if constexpr (MM == 3) on = ((zbits >> q) & 1u) != 0u;
-            const float g = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
-            a.v[q] = g;
-            bsg[q] += g;
-            bsq[q] = fmaf(g, yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
+            bsg[q] += a.v[q];
+            bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
           }
-          v = __builtin_bit_cast(v4i, pack8(a));
         }
         if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
       }
@@ -854,15 +887,20 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   using HT = std::integral_constant<bool, true>;
   using HF = std::integral_constant<bool, false>;
   const bool has_add = P.addend != nullptr;
+  const bool dense = P.dense && !(has_add && P.add_sub);
+  auto with_dn = [&](auto mm, auto ha) {
+    if (dense) run_batches(mm, ha, HT{});
+    else run_batches(mm, ha, HF{});
+  };
   if constexpr (EPI == EPI_BNB) {
     switch (P.bn_mask) {
-      case 1: if (has_add) run_batches(M1{}, HT{}); else run_batches(M1{}, HF{}); break;
-      case 2: if (has_add) run_batches(M2{}, HT{}); else run_batches(M2{}, HF{}); break;
-      case 3: if (has_add) run_batches(M3{}, HT{}); else run_batches(M3{}, HF{}); break;
-      default: if (has_add) run_batches(M0{}, HT{}); else run_batches(M0{}, HF{}); break;
+      case 1: if (has_add) with_dn(M1{}, HT{}); else with_dn(M1{}, HF{}); break;
+      case 2: if (has_add) with_dn(M2{}, HT{}); else with_dn(M2{}, HF{}); break;
+      case 3: if (has_add) with_dn(M3{}, HT{}); else with_dn(M3{}, HF{}); break;
+      default: if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{}); break;
     }
   } else {
-    if (has_add) run_batches(M0{}, HT{}); else run_batches(M0{}, HF{});
+    if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{});
   }
   if constexpr (EPI == EPI_BNB) {
     // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
