@@ -254,6 +254,350 @@ constexpr int nt_min_waves() {
   return WAVES == 4 ? (HALO ? 2 : PDT_NT_OCC4) : PDT_NT_OCC8;
 }
 
+// NT epilogue (a device function so other NT-shaped kernels can share it): BN
+// statistics (EPI_STATS) or the fused BN-backward mask / partial sums (EPI_BNB), bf16 staging
+// through LDS (`smem`, idle pipeline buffers: every wave must be past its last fragment read)
+// and 16-byte row stores.  Every thread of the workgroup calls it (it has block barriers).
+template <class CFG, int WM, int WN, int TM, int TN, int EPI, int OP>
+__device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN], char* smem, int m0, int n0,
+                                            int tmi) {
+  constexpr int BM = CFG::BM, BN = CFG::BN;
+  (void)BM;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wid % WM, wn = wid / WM;
+  const int fr = lane & 15, fq = lane >> 4;
+  // lane (fq, fr), register e of acc[i][j]: pixel i*16 + fr, channel j*16 + fq*4 + e
+  const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
+  const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
+
+  if constexpr (OP != OP_BF16) {
+    // fp8: back to real units with the per-column factor (weight scale x activation scale)
+    const float as = P.ascale != nullptr ? P.ascale[0] : 1.f;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wcol0 + j * 16 + fq * 4;
+      float4 sc = col < P.Nout ? *reinterpret_cast<const float4*>(P.oscale + col)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      sc.x *= as; sc.y *= as; sc.z *= as; sc.w *= as;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[i][j][0] *= sc.x; acc[i][j][1] *= sc.y; acc[i][j][2] *= sc.z; acc[i][j][3] *= sc.w;
+      }
+    }
+  }
+
+  if constexpr (EPI == EPI_STATS) {
+    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels,
+    // converted to M2 about the wave's mean (cancellation is benign at <= 64 rows).  The WM wave
+    // rows of the workgroup are then merged in LDS (Chan: M2 = sum M2_w + sum n_w (mean_w -
+    // mean)^2), so ONE partial per (workgroup row tile, channel) goes out and bn_finalize reads
+    // BM-row groups (4x fewer partials on the 256-row tiles than per-wave groups).
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]: the pipeline buffers are idle now
+    const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
+    {
+      const bool full = valid == TM * 16;  // wave-uniform: no per-element masking on full tiles
+      const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s[4], q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = 0.f, v2 = 0.f;
+          if (full) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              v += acc[i][j][e];
+              v2 = fmaf(acc[i][j][e], acc[i][j][e], v2);
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
+              v += a;
+              v2 = fmaf(a, a, v2);
+            }
+          }
+          v = row_sum16(v);    // the 16 lanes of a DPP row are the 16 pixels of a tile row
+          v2 = row_sum16(v2);
+          s[e] = v;
+          q[e] = fmaxf(v2 - v * v * inv_valid, 0.f);
+        }
+        if (fr == 0) {
+          const int cl = wn * TN * 16 + j * 16 + fq * 4;  // column within the workgroup tile
+          *reinterpret_cast<float4*>(red + (wm * 2 + 0) * BN + cl) = make_float4(s[0], s[1], s[2], s[3]);
+          *reinterpret_cast<float4*>(red + (wm * 2 + 1) * BN + cl) = make_float4(q[0], q[1], q[2], q[3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
+      float sw[WM], qw[WM], nw[WM];
+      float S = 0.f, Nr = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        nw[w] = (float)max(0, min(TM * 16, P.M - (m0 + w * TM * 16)));
+        sw[w] = red[(w * 2 + 0) * BN + t];
+        qw[w] = red[(w * 2 + 1) * BN + t];
+        S += sw[w];
+        Nr += nw[w];
+      }
+      const float mean = S / Nr;  // Nr > 0: the tile's first wave row is inside the GEMM
+      float Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        if (nw[w] > 0.f) {
+          const float d = sw[w] / nw[w] - mean;
+          Q += qw[w] + nw[w] * d * d;
+        }
+      }
+      const int col = n0 + t;
+      if (col < P.Nout) {
+        P.part[((int64_t)tmi * 2 + 0) * P.Nout + col] = S;
+        P.part[((int64_t)tmi * 2 + 1) * P.Nout + col] = Q;
+      }
+    }
+    __syncthreads();  // red[] aliases the staging rows written next
+  }
+
+  // stage the wave's pixels x channels tile as bf16 (8-byte writes), then 16-byte row stores
+  char* ep = smem + wid * (TM * 16) * CFG::EPI_PITCH;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      uint2 v;
+      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(ep + (i * 16 + fr) * CFG::EPI_PITCH + (j * 16 + fq * 4) * 2) = v;
+    }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region is wave-private, no barrier needed
+  __builtin_amdgcn_wave_barrier();
+  constexpr int CH_PER_ROW = TN * 2;  // 16-B chunks per wave-tile row
+  constexpr int CHUNKS = TM * 16 * CH_PER_ROW;
+  static_assert(64 % CH_PER_ROW == 0, "a lane keeps one channel chunk across the store loop");
+  // EPI_BNB: this lane's 8 channels are fixed (c = lane % CH_PER_ROW); per-lane partial sums
+  float bmu[8], bsc[8], bsh[8], bsg[8], bsq[8];
+  if constexpr (EPI == EPI_BNB) {
+    const int colb = min(wcol0 + (lane % CH_PER_ROW) * 8, P.Nout - 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      bmu[q] = P.bn_stats[colb + q];
+      bsc[q] = P.bn_stats[2 * P.Nout + colb + q];
+      bsh[q] = P.bn_stats[3 * P.Nout + colb + q];
+      bsg[q] = 0.f;
+      bsq[q] = 0.f;
+    }
+  }
+  // Two phases per batch of up to 8 chunks: first issue every global read the epilogue needs
+  // (BN y / z, residual-gradient addend) -- bounds-checked buffer loads, OOB lanes read 0 --
+  // then combine and store.  One exposed memory latency per batch instead of one per chunk (the
+  // compiler cannot hoist a load above a store that may alias it); batches bound the registers.
+  constexpr int IT_ALL = CHUNKS / 64;
+#ifndef PDT_EPI_IT
+#define PDT_EPI_IT 8
+#endif
+  constexpr int IT_MAX = PDT_EPI_IT;  // (y, z, addend) chunks in flight per lane and batch
+  constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
+  static_assert(IT_ALL % IT == 0, "chunk batches");
+  // The BN mask mode, the addend and the output addressing are wave-uniform: dispatch ONCE to a
+  // copy of the batch loop specialised on them (per-element tests of kernel arguments cost ~6x
+  // the SALU and 2.5x the VALU instructions of the plain epilogue, measured).
+  //   DN: dense output (GEMM row == NHWC pixel) and, if any, an addend at the same offsets -- a
+  //       chunk's offset is then the lane's base + a compile-time multiple of the row pitch (one
+  //       add and one compare per chunk instead of the pixel decomposition's ~12 VALU).
+  // Mask mode 3 (bitmask) masks the PACKED bf16 chunk: per pair of channels two sign-extended
+  // bit fields merged by one v_bfi_b32 give the 32-bit keep-mask, so g is never unpacked, masked
+  // and re-packed (the chunk was rounded to bf16 already: same bits as masking in fp32).
+  auto run_batches = [&](auto mm_c, auto ha_c, auto dn_c) {
+    constexpr int MM = decltype(mm_c)::value;   // 0 none, 1 z > 0, 2 y*sc+sh > 0, 3 bitmask
+    constexpr bool HA = decltype(ha_c)::value;  // residual-gradient addend
+    constexpr bool DN = decltype(dn_c)::value;  // dense addressing fast path
+    constexpr int RSTEP = 64 / CH_PER_ROW;      // staging rows advanced per chunk slot
+    const int c_l = lane % CH_PER_ROW, r_l = lane / CH_PER_ROW;
+    const int col_l = wcol0 + c_l * 8;
+    const int mrem = (col_l < P.Nout) ? P.M - (wrow0 + r_l) : 0;  // rows this lane may still touch
+    const uint32_t off_l = ((uint32_t)(wrow0 + r_l) * (uint32_t)P.Nout + (uint32_t)col_l) * 2u;
+    const uint32_t pitch = (uint32_t)P.Nout * 2u * RSTEP;  // bytes between a lane's chunks
+#pragma unroll 1
+    for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
+      uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
+      uint32_t aoff[IT];  // byte offset of the chunk in a compact (stride-2) addend, or OOB
+      if constexpr (DN) {
+        const uint32_t ob = off_l + (uint32_t)b0 * pitch;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          ooff[it] = (b0 + it) * RSTEP < mrem ? ob + (uint32_t)it * pitch : OOB;
+          aoff[it] = ooff[it];
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          const int qd = lane + (b0 + it) * 64;
+          const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+          const int m = wrow0 + r;
+          const int col = wcol0 + c * 8;
+          ooff[it] = OOB;
+          aoff[it] = OOB;
+          if (m < P.M && col < P.Nout) {
+            // 32-bit offsets: every operand is addressed through a buffer resource (< 4 GiB)
+            uint32_t orow = (uint32_t)m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel
+            if (!P.dense || (HA && P.add_sub)) {
+              uint32_t n = fdiv((uint32_t)m, P.div_ij);
+              uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+              uint32_t ii = fdiv(rem, P.div_j);
+              uint32_t jj = rem - ii * (uint32_t)P.Mj;
+              if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
+                orow = (n * (uint32_t)P.OH + ii * (uint32_t)P.osh + (uint32_t)P.oph) * (uint32_t)P.OW +
+                       jj * (uint32_t)P.osw + (uint32_t)P.opw;
+              if (HA && P.add_sub) {
+                // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
+                // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
+                const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
+                const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
+                if (((hh | ww) & 1) == 0)
+                  aoff[it] = (((n * (uint32_t)P.add_h + (uint32_t)(hh >> 1)) * (uint32_t)P.add_w + (uint32_t)(ww >> 1)) *
+                                  (uint32_t)P.Nout + (uint32_t)col) * 2u;
+              }
+            }
+            ooff[it] = (orow * (uint32_t)P.Nout + (uint32_t)col) * 2u;
+            if (HA && !P.add_sub) aoff[it] = ooff[it];
+          }
+        }
+      }
+      v4i av[IT], yv[IT], zv[IT];
+      if constexpr (HA) {
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.add_bytes);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, aoff[it]);
+      }
+      if constexpr (EPI == EPI_BNB) {
+        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
+        if constexpr (MM == 1) {
+          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
+#pragma unroll
+          for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
+        } else if constexpr (MM == 3) {  // 1 byte per 16-B chunk instead of the 16-B z chunk
+          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes >> 4);
+#pragma unroll
+          for (int it = 0; it < IT; ++it)
+            zv[it][0] = (int)__builtin_amdgcn_raw_buffer_load_b8(rz, ooff[it] == OOB ? OOB : ooff[it] >> 4, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int qd = lane + (b0 + it) * 64;
+        const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
+        v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+        if constexpr (HA) {  // fused residual-gradient sum (block input of a residual block)
+          f8 a = unpack8(__builtin_bit_cast(uint4, v));
+          const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
+          v = __builtin_bit_cast(v4i, pack8(a));
+        }
+        if constexpr (EPI == EPI_BNB) {
+          // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
+          // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
+          // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
+          if constexpr (MM == 3) {
+            const int zb = zv[it][0];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h, 1);      // 0 or ~0
+              const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h + 1, 1);
+              const uint32_t keep = (0x0000ffffu & lo) | (~0x0000ffffu & hi);         // v_bfi_b32
+              v[h] = (int)((uint32_t)v[h] & keep);
+            }
+          }
+          f8 a = unpack8(__builtin_bit_cast(uint4, v));
+          const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
+          if constexpr (MM == 1 || MM == 2) {
+            f8 zz;
+            if constexpr (MM == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              bool on;
+              if constexpr (MM == 1) on = zz.v[q] > 0.f;
+              else on = fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f;
+              a.v[q] = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
+            }
+            v = __builtin_bit_cast(v4i, pack8(a));
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            bsg[q] += a.v[q];
+            bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
+          }
+        }
+        if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
+      }
+    }
+  };
+  using M0 = std::integral_constant<int, 0>;
+  using M1 = std::integral_constant<int, 1>;
+  using M2 = std::integral_constant<int, 2>;
+  using M3 = std::integral_constant<int, 3>;
+  using HT = std::integral_constant<bool, true>;
+  using HF = std::integral_constant<bool, false>;
+  const bool has_add = P.addend != nullptr;
+  const bool dense = P.dense && !(has_add && P.add_sub);
+  auto with_dn = [&](auto mm, auto ha) {
+    if (dense) run_batches(mm, ha, HT{});
+    else run_batches(mm, ha, HF{});
+  };
+  if constexpr (EPI == EPI_BNB) {
+    switch (P.bn_mask) {
+      case 1: if (has_add) with_dn(M1{}, HT{}); else with_dn(M1{}, HF{}); break;
+      case 2: if (has_add) with_dn(M2{}, HT{}); else with_dn(M2{}, HF{}); break;
+      case 3: if (has_add) with_dn(M3{}, HT{}); else with_dn(M3{}, HF{}); break;
+      default: if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{}); break;
+    }
+  } else {
+    if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{});
+  }
+  if constexpr (EPI == EPI_BNB) {
+    // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
+    // loop above (the epilogue, not the MFMAs, bounds the short-K dgrads' issue)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bsq[q] = fmaf(-bmu[q], bsg[q], bsq[q]);
+    // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
+    // first CH_PER_ROW lanes write this wave's (rows group, channels) partials
+#pragma unroll
+    for (int o = CH_PER_ROW; o < 64; o <<= 1)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        bsg[q] += __shfl_xor(bsg[q], o, 64);
+        bsq[q] += __shfl_xor(bsq[q], o, 64);
+      }
+    // then the WM wave rows of the workgroup are summed in LDS (fixed order): one partial per
+    // (workgroup row tile, channel).  Waves past the GEMM edge hold zeros.
+    __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    if (lane < CH_PER_ROW) {
+      float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
+      *reinterpret_cast<float4*>(rp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
+      *reinterpret_cast<float4*>(rp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
+      *reinterpret_cast<float4*>(rp + BN) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
+      *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
+    }
+    __syncthreads();
+    if (t < BN && n0 + t < P.Nout) {
+      float S = 0.f, Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        S += red[(w * 2) * BN + t];
+        Q += red[(w * 2 + 1) * BN + t];
+      }
+      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + tmi) * 2) * P.Nout + n0 + t;
+      pp[0] = S;
+      pp[P.Nout] = Q;
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int STAGES, bool C64, int EPI, int OP = OP_BF16, bool HALO = false,
           bool K32 = false>
 __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>())) igemm_nt_kernel(const NtArgs P) {
@@ -611,336 +955,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   }  // !HALO
 
   // --------------------------------------------------------------- epilogue
-  // lane (fq, fr), register e of acc[i][j]: pixel i*16 + fr, channel j*16 + fq*4 + e
-  const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
-  const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
-
-  if constexpr (OP != OP_BF16) {
-    // fp8: back to real units with the per-column factor (weight scale x activation scale)
-    const float as = P.ascale != nullptr ? P.ascale[0] : 1.f;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wcol0 + j * 16 + fq * 4;
-      float4 sc = col < P.Nout ? *reinterpret_cast<const float4*>(P.oscale + col)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-      sc.x *= as; sc.y *= as; sc.z *= as; sc.w *= as;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        acc[i][j][0] *= sc.x; acc[i][j][1] *= sc.y; acc[i][j][2] *= sc.z; acc[i][j][3] *= sc.w;
-      }
-    }
-  }
-
-  if constexpr (EPI == EPI_STATS) {
-    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels,
-    // converted to M2 about the wave's mean (cancellation is benign at <= 64 rows).  The WM wave
-    // rows of the workgroup are then merged in LDS (Chan: M2 = sum M2_w + sum n_w (mean_w -
-    // mean)^2), so ONE partial per (workgroup row tile, channel) goes out and bn_finalize reads
-    // BM-row groups (4x fewer partials on the 256-row tiles than per-wave groups).
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]: the pipeline buffers are idle now
-    const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
-    {
-      const bool full = valid == TM * 16;  // wave-uniform: no per-element masking on full tiles
-      const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float s[4], q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = 0.f, v2 = 0.f;
-          if (full) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-              v += acc[i][j][e];
-              v2 = fmaf(acc[i][j][e], acc[i][j][e], v2);
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-              const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
-              v += a;
-              v2 = fmaf(a, a, v2);
-            }
-          }
-          v = row_sum16(v);    // the 16 lanes of a DPP row are the 16 pixels of a tile row
-          v2 = row_sum16(v2);
-          s[e] = v;
-          q[e] = fmaxf(v2 - v * v * inv_valid, 0.f);
-        }
-        if (fr == 0) {
-          const int cl = wn * TN * 16 + j * 16 + fq * 4;  // column within the workgroup tile
-          *reinterpret_cast<float4*>(red + (wm * 2 + 0) * BN + cl) = make_float4(s[0], s[1], s[2], s[3]);
-          *reinterpret_cast<float4*>(red + (wm * 2 + 1) * BN + cl) = make_float4(q[0], q[1], q[2], q[3]);
-        }
-      }
-    }
-    __syncthreads();
-    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
-      float sw[WM], qw[WM], nw[WM];
-      float S = 0.f, Nr = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        nw[w] = (float)max(0, min(TM * 16, P.M - (m0 + w * TM * 16)));
-        sw[w] = red[(w * 2 + 0) * BN + t];
-        qw[w] = red[(w * 2 + 1) * BN + t];
-        S += sw[w];
-        Nr += nw[w];
-      }
-      const float mean = S / Nr;  // Nr > 0: the tile's first wave row is inside the GEMM
-      float Q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        if (nw[w] > 0.f) {
-          const float d = sw[w] / nw[w] - mean;
-          Q += qw[w] + nw[w] * d * d;
-        }
-      }
-      const int col = n0 + t;
-      if (col < P.Nout) {
-        P.part[((int64_t)tmi * 2 + 0) * P.Nout + col] = S;
-        P.part[((int64_t)tmi * 2 + 1) * P.Nout + col] = Q;
-      }
-    }
-    __syncthreads();  // red[] aliases the staging rows written next
-  }
-
-  // stage the wave's pixels x channels tile as bf16 (8-byte writes), then 16-byte row stores
-  char* ep = smem + wid * (TM * 16) * CFG::EPI_PITCH;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      uint2 v;
-      v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
-      v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(ep + (i * 16 + fr) * CFG::EPI_PITCH + (j * 16 + fq * 4) * 2) = v;
-    }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region is wave-private, no barrier needed
-  __builtin_amdgcn_wave_barrier();
-  constexpr int CH_PER_ROW = TN * 2;  // 16-B chunks per wave-tile row
-  constexpr int CHUNKS = TM * 16 * CH_PER_ROW;
-  static_assert(64 % CH_PER_ROW == 0, "a lane keeps one channel chunk across the store loop");
-  // EPI_BNB: this lane's 8 channels are fixed (c = lane % CH_PER_ROW); per-lane partial sums
-  float bmu[8], bsc[8], bsh[8], bsg[8], bsq[8];
-  if constexpr (EPI == EPI_BNB) {
-    const int colb = min(wcol0 + (lane % CH_PER_ROW) * 8, P.Nout - 8);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      bmu[q] = P.bn_stats[colb + q];
-      bsc[q] = P.bn_stats[2 * P.Nout + colb + q];
-      bsh[q] = P.bn_stats[3 * P.Nout + colb + q];
-      bsg[q] = 0.f;
-      bsq[q] = 0.f;
-    }
-  }
-  // Two phases per batch of up to 8 chunks: first issue every global read the epilogue needs
-  // (BN y / z, residual-gradient addend) -- bounds-checked buffer loads, OOB lanes read 0 --
-  // then combine and store.  One exposed memory latency per batch instead of one per chunk (the
-  // compiler cannot hoist a load above a store that may alias it); batches bound the registers.
-  constexpr int IT_ALL = CHUNKS / 64;
-#ifndef PDT_EPI_IT
-#define PDT_EPI_IT 8
-#endif
-  constexpr int IT_MAX = PDT_EPI_IT;  // (y, z, addend) chunks in flight per lane and batch
-  constexpr int IT = IT_ALL < IT_MAX ? IT_ALL : IT_MAX;
-  static_assert(IT_ALL % IT == 0, "chunk batches");
-  // The BN mask mode, the addend and the output addressing are wave-uniform: dispatch ONCE to a
-  // copy of the batch loop specialised on them (per-element tests of kernel arguments cost ~6x
-  // the SALU and 2.5x the VALU instructions of the plain epilogue, measured).
-  //   DN: dense output (GEMM row == NHWC pixel) and, if any, an addend at the same offsets -- a
-  //       chunk's offset is then the lane's base + a compile-time multiple of the row pitch (one
-  //       add and one compare per chunk instead of the pixel decomposition's ~12 VALU).
-  // Mask mode 3 (bitmask) masks the PACKED bf16 chunk: per pair of channels two sign-extended
-  // bit fields merged by one v_bfi_b32 give the 32-bit keep-mask, so g is never unpacked, masked
-  // and re-packed (the chunk was rounded to bf16 already: same bits as masking in fp32).
-  auto run_batches = [&](auto mm_c, auto ha_c, auto dn_c) {
-    constexpr int MM = decltype(mm_c)::value;   // 0 none, 1 z > 0, 2 y*sc+sh > 0, 3 bitmask
-    constexpr bool HA = decltype(ha_c)::value;  // residual-gradient addend
-    constexpr bool DN = decltype(dn_c)::value;  // dense addressing fast path
-    constexpr int RSTEP = 64 / CH_PER_ROW;      // staging rows advanced per chunk slot
-    const int c_l = lane % CH_PER_ROW, r_l = lane / CH_PER_ROW;
-    const int col_l = wcol0 + c_l * 8;
-    const int mrem = (col_l < P.Nout) ? P.M - (wrow0 + r_l) : 0;  // rows this lane may still touch
-    const uint32_t off_l = ((uint32_t)(wrow0 + r_l) * (uint32_t)P.Nout + (uint32_t)col_l) * 2u;
-    const uint32_t pitch = (uint32_t)P.Nout * 2u * RSTEP;  // bytes between a lane's chunks
-#pragma unroll 1
-    for (int b0 = 0; b0 < IT_ALL; b0 += IT) {
-      uint32_t ooff[IT];  // byte offset of the chunk in the NHWC output (and y / z / addend), or OOB
-      uint32_t aoff[IT];  // byte offset of the chunk in a compact (stride-2) addend, or OOB
-      if constexpr (DN) {
-        const uint32_t ob = off_l + (uint32_t)b0 * pitch;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          ooff[it] = (b0 + it) * RSTEP < mrem ? ob + (uint32_t)it * pitch : OOB;
-          aoff[it] = ooff[it];
-        }
-      } else {
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          const int qd = lane + (b0 + it) * 64;
-          const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-          const int m = wrow0 + r;
-          const int col = wcol0 + c * 8;
-          ooff[it] = OOB;
-          aoff[it] = OOB;
-          if (m < P.M && col < P.Nout) {
-            // 32-bit offsets: every operand is addressed through a buffer resource (< 4 GiB)
-            uint32_t orow = (uint32_t)m;  // dense output (fwd, stride-1 dgrad): GEMM row == NHWC pixel
-            if (!P.dense || (HA && P.add_sub)) {
-              uint32_t n = fdiv((uint32_t)m, P.div_ij);
-              uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
-              uint32_t ii = fdiv(rem, P.div_j);
-              uint32_t jj = rem - ii * (uint32_t)P.Mj;
-              if (!P.dense)    // parity-class dgrad: scatter to (n, i*s + ph, j*s + pw)
-                orow = (n * (uint32_t)P.OH + ii * (uint32_t)P.osh + (uint32_t)P.oph) * (uint32_t)P.OW +
-                       jj * (uint32_t)P.osw + (uint32_t)P.opw;
-              if (HA && P.add_sub) {
-                // compact addend: (n, h/2, w/2) for even h and w.  Parity class (0, 0) of a stride-2
-                // dgrad IS that grid (row m -> compact pixel m); other classes get nothing
-                const int hh = P.dense ? (int)ii : (int)ii * P.osh + P.oph;
-                const int ww = P.dense ? (int)jj : (int)jj * P.osw + P.opw;
-                if (((hh | ww) & 1) == 0)
-                  aoff[it] = (((n * (uint32_t)P.add_h + (uint32_t)(hh >> 1)) * (uint32_t)P.add_w + (uint32_t)(ww >> 1)) *
-                                  (uint32_t)P.Nout + (uint32_t)col) * 2u;
-              }
-            }
-            ooff[it] = (orow * (uint32_t)P.Nout + (uint32_t)col) * 2u;
-            if (HA && !P.add_sub) aoff[it] = ooff[it];
-          }
-        }
-      }
-      v4i av[IT], yv[IT], zv[IT];
-      if constexpr (HA) {
-        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.add_bytes);
-#pragma unroll
-        for (int it = 0; it < IT; ++it) av[it] = buf_load16(rr, aoff[it]);
-      }
-      if constexpr (EPI == EPI_BNB) {
-        const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
-#pragma unroll
-        for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
-        if constexpr (MM == 1) {
-          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
-#pragma unroll
-          for (int it = 0; it < IT; ++it) zv[it] = buf_load16(rz, ooff[it]);
-        } else if constexpr (MM == 3) {  // 1 byte per 16-B chunk instead of the 16-B z chunk
-          const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes >> 4);
-#pragma unroll
-          for (int it = 0; it < IT; ++it)
-            zv[it][0] = (int)__builtin_amdgcn_raw_buffer_load_b8(rz, ooff[it] == OOB ? OOB : ooff[it] >> 4, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int qd = lane + (b0 + it) * 64;
-        const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-        v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
-        if constexpr (HA) {  // fused residual-gradient sum (block input of a residual block)
-          f8 a = unpack8(__builtin_bit_cast(uint4, v));
-          const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
-#pragma unroll
-          for (int q = 0; q < 8; ++q) a.v[q] += b.v[q];
-          v = __builtin_bit_cast(v4i, pack8(a));
-        }
-        if constexpr (EPI == EPI_BNB) {
-          // g = dx * relu'(unit output); g is bf16-exact (dx or 0), so the stored tensor and the
-          // partial sums agree bit for bit with what the apply pass reads back.  OOB chunks read
-          // y = 0 and contribute g = 0 (their accumulators are 0: rows/cols past the GEMM edge).
-          if constexpr (MM == 3) {
-            const int zb = zv[it][0];
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h, 1);      // 0 or ~0
-              const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe(zb, 2 * h + 1, 1);
-              const uint32_t keep = (0x0000ffffu & lo) | (~0x0000ffffu & hi);         // v_bfi_b32
-              v[h] = (int)((uint32_t)v[h] & keep);
-            }
-          }
-          f8 a = unpack8(__builtin_bit_cast(uint4, v));
-          const f8 yy = unpack8(__builtin_bit_cast(uint4, yv[it]));
-          if constexpr (MM == 1 || MM == 2) {
-            f8 zz;
-            if constexpr (MM == 1) zz = unpack8(__builtin_bit_cast(uint4, zv[it]));
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              bool on;
-              if constexpr (MM == 1) on = zz.v[q] > 0.f;
-              else on = fmaf(yy.v[q], bsc[q], bsh[q]) > 0.f;
-              a.v[q] = on ? a.v[q] : 0.f;  // OOB: a == 0 and y == 0 -> contributes 0
-            }
-            v = __builtin_bit_cast(v4i, pack8(a));
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            bsg[q] += a.v[q];
-            bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
-          }
-        }
-        if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
-      }
-    }
-  };
-  using M0 = std::integral_constant<int, 0>;
-  using M1 = std::integral_constant<int, 1>;
-  using M2 = std::integral_constant<int, 2>;
-  using M3 = std::integral_constant<int, 3>;
-  using HT = std::integral_constant<bool, true>;
-  using HF = std::integral_constant<bool, false>;
-  const bool has_add = P.addend != nullptr;
-  const bool dense = P.dense && !(has_add && P.add_sub);
-  auto with_dn = [&](auto mm, auto ha) {
-    if (dense) run_batches(mm, ha, HT{});
-    else run_batches(mm, ha, HF{});
-  };
-  if constexpr (EPI == EPI_BNB) {
-    switch (P.bn_mask) {
-      case 1: if (has_add) with_dn(M1{}, HT{}); else with_dn(M1{}, HF{}); break;
-      case 2: if (has_add) with_dn(M2{}, HT{}); else with_dn(M2{}, HF{}); break;
-      case 3: if (has_add) with_dn(M3{}, HT{}); else with_dn(M3{}, HF{}); break;
-      default: if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{}); break;
-    }
-  } else {
-    if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{});
-  }
-  if constexpr (EPI == EPI_BNB) {
-    // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
-    // loop above (the epilogue, not the MFMAs, bounds the short-K dgrads' issue)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) bsq[q] = fmaf(-bmu[q], bsg[q], bsq[q]);
-    // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
-    // first CH_PER_ROW lanes write this wave's (rows group, channels) partials
-#pragma unroll
-    for (int o = CH_PER_ROW; o < 64; o <<= 1)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        bsg[q] += __shfl_xor(bsg[q], o, 64);
-        bsq[q] += __shfl_xor(bsq[q], o, 64);
-      }
-    // then the WM wave rows of the workgroup are summed in LDS (fixed order): one partial per
-    // (workgroup row tile, channel).  Waves past the GEMM edge hold zeros.
-    __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
-    if (lane < CH_PER_ROW) {
-      float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
-      *reinterpret_cast<float4*>(rp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
-      *reinterpret_cast<float4*>(rp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
-      *reinterpret_cast<float4*>(rp + BN) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
-      *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
-    }
-    __syncthreads();
-    if (t < BN && n0 + t < P.Nout) {
-      float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        S += red[(w * 2) * BN + t];
-        Q += red[(w * 2 + 1) * BN + t];
-      }
-      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + tmi) * 2) * P.Nout + n0 + t;
-      pp[0] = S;
-      pp[P.Nout] = Q;
-    }
-  }
+  nt_epilogue<CFG, WM, WN, TM, TN, EPI, OP>(P, acc, smem, m0, n0, tmi);
 }
+
 
 // ============================================================================
 //                      TN implicit GEMM (wgrad, split-K)
