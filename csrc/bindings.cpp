@@ -780,8 +780,10 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, int64_t H, int64_t W) {
   return dx;
 }
 
-// stem: (pooled, idx) = maxpool3x3s2(relu(y*scale + shift)) without writing the ReLU output
-std::tuple<Tensor, Tensor> bn_relu_maxpool(const Tensor& y, const Tensor& scale, const Tensor& shift) {
+// stem: (pooled, idx) = maxpool3x3s2(relu(y*scale + shift)) without writing the ReLU output;
+// with argmax_y also u = y at each window's argmax (what the BN backward reduction needs from y:
+// it then streams the pooled tensors instead of gathering over the full-resolution y)
+py::tuple bn_relu_maxpool(const Tensor& y, const Tensor& scale, const Tensor& shift, bool argmax_y) {
   check_bf16_nhwc(y, "y");
   check_cuda(scale, "scale");
   check_cuda(shift, "shift");
@@ -792,9 +794,13 @@ std::tuple<Tensor, Tensor> bn_relu_maxpool(const Tensor& y, const Tensor& scale,
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   auto out = at::empty({N, Ho, Wo, C}, y.options());
   auto idx = at::empty({N, Ho, Wo, C}, y.options().dtype(at::kByte));
+  Tensor u;
+  if (argmax_y) u = at::empty({N, Ho, Wo, C}, y.options());
   pdt::launch_bn_relu_maxpool(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), bf(out),
-                              idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, cur_stream(y));
-  return {out, idx};
+                              idx.data_ptr<uint8_t>(), argmax_y ? bf(u) : nullptr, N, H, W, C, Ho, Wo,
+                              cur_stream(y));
+  if (argmax_y) return py::make_tuple(out, idx, u);
+  return py::make_tuple(out, idx);
 }
 
 static void check_pool_grad(const Tensor& dpool, const Tensor& idx, const Tensor& y) {
@@ -1205,7 +1211,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("flip"), py::arg("pad"), py::arg("normalize"), py::arg("mean"), py::arg("std"));
   m.def("maxpool_fwd", checked("maxpool_fwd", &maxpool_fwd));
   m.def("maxpool_bwd", checked("maxpool_bwd", &maxpool_bwd));
-  m.def("bn_relu_maxpool", checked("bn_relu_maxpool", &bn_relu_maxpool));
+  m.def("bn_relu_maxpool", checked("bn_relu_maxpool", &bn_relu_maxpool), py::arg("y"), py::arg("scale"),
+        py::arg("shift"), py::arg("argmax_y") = false);
   m.def("pool_bn_bwd_reduce", checked("pool_bn_bwd_reduce", &pool_bn_bwd_reduce), py::arg("dpool"),
         py::arg("idx"), py::arg("y"), py::arg("stats"), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none());

@@ -741,7 +741,8 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
                                                               uint4* __restrict__ out,
-                                                              uint2* __restrict__ idx, uint32_t total,
+                                                              uint2* __restrict__ idx,
+                                                              uint4* __restrict__ uarg, uint32_t total,
                                                               int H, int W, int lc8, int Ho, int Wo) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
@@ -752,10 +753,10 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
   float sc[8], sh[8];
   load8(scale + c8 * 8, sc);
   load8(shift + c8 * 8, sh);
-  float best[8];
+  float best[8], ub[8];
   uint32_t bi[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; ub[j] = 0.f; }
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int h = ho * 2 - 1 + kh;
@@ -768,7 +769,7 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float z = bf16_round(fmaxf(fmaf(v.v[j], sc[j], sh[j]), 0.f));
-        if (z > best[j] || __builtin_isnan(z)) { best[j] = z; bi[j] = (uint32_t)(kh * 3 + kw); }
+        if (z > best[j] || __builtin_isnan(z)) { best[j] = z; bi[j] = (uint32_t)(kh * 3 + kw); ub[j] = v.v[j]; }
       }
     }
   }
@@ -778,6 +779,12 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
   out[t] = pack8(o);
   idx[t] = make_uint2(bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
                       bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24));
+  if (uarg != nullptr) {  // the pre-BN value at the argmax (bf16-exact: a copy of y's element)
+    f8 u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u.v[j] = ub[j];
+    uarg[t] = pack8(u);
+  }
 }
 
 // stage 1 of the stem BN backward reduction, dz gathered per quad from the pooled gradient
@@ -895,14 +902,16 @@ static int log2_exact(int v) {
 }
 
 void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* shift, uint16_t* out,
-                            uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st) {
+                            uint8_t* idx, uint16_t* uarg, int N, int H, int W, int C, int Ho, int Wo,
+                            hipStream_t st) {
   check_pool_bn_channels(C);
   const int C8 = C / 8;
   const int64_t total = (int64_t)N * Ho * Wo * C8;
   if ((int64_t)N * H * W * C8 >= (int64_t)1 << 31) throw std::runtime_error("bn_relu_maxpool: tensor too large");
   hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const uint4*>(y), scale, shift, reinterpret_cast<uint4*>(out),
-                     reinterpret_cast<uint2*>(idx), (uint32_t)total, H, W, log2_exact(C8), Ho, Wo);
+                     reinterpret_cast<uint2*>(idx), reinterpret_cast<uint4*>(uarg), (uint32_t)total, H, W,
+                     log2_exact(C8), Ho, Wo);
 }
 
 // The stem's fused pool/BN reduction gathers each 2x2 quad's pooled gradient (dependent loads)

@@ -145,7 +145,8 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
 // bf16 z, which is never written.  Backward: the BN reduction / apply with dz gathered from the
 // pooled gradient (mask mode 2); ws >= pool_bn_bwd_ws_floats(N*H*W, K).  K <= 256.
 void launch_bn_relu_maxpool(const uint16_t* y, const float* scale, const float* shift, uint16_t* out,
-                            uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
+                            uint8_t* idx, uint16_t* uarg, int N, int H, int W, int C, int Ho, int Wo,
+                            hipStream_t st);
 size_t pool_bn_bwd_ws_floats(int64_t M, int K);
 void launch_pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* idx, const uint16_t* y,
                                const float* stats, int N, int H, int W, int K, int Ho, int Wo,

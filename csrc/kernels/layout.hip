@@ -89,13 +89,15 @@ void launch_pack_weight_t(const float* w, const int64_t* strides, uint16_t* out,
 // slice src[off .. off + K*RS*C) (written by the fused SGD step) is transposed to CRSK at
 // dst[off ..].  One launch for all layers: blockIdx.y = tensor, blockIdx.x walks that tensor's
 // (tap, 64-k, 64-c) tiles; a 64x64 tile goes through LDS so reads (c-contiguous) and writes
-// (k-contiguous) are both 16-B vectors.
+// (k-contiguous) are both 16-B vectors.  Row pitch 66 halves (33 dwords): the transposed gather
+// (lane (k-chunk m, c row r) reads tile[8m + q][r]) lands on banks 8m + r/2 + 33q -- distinct
+// for the 8 k-chunks (the 72-half pitch put chunks m and m+2 on one bank: 4-way conflicts).
 struct PackTEntry { int64_t off; int K, C, RS, tiles_k, tiles_c; };
 
 __global__ void __launch_bounds__(256) pack_t_batched_kernel(const uint16_t* __restrict__ src,
                                                              uint16_t* __restrict__ dst,
                                                              const PackTEntry* __restrict__ tab) {
-  __shared__ uint16_t tile[64][64 + 8];
+  __shared__ uint16_t tile[64][66];
   const PackTEntry e = tab[blockIdx.y];
   const int per_tap = e.tiles_k * e.tiles_c;
   const int ntiles = e.RS * per_tap;

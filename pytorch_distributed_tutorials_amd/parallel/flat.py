@@ -217,6 +217,7 @@ class WeightMirror:
         if self.key8 != self.key or torch.cuda.is_current_stream_capturing():
             from ..ops._ext import native
             C, f = native(), self._fp8
+            self._join_pack()  # reads crsk
             C.quant_rows_e4m3(self.krsc, f["krsc8"], f["kscale"], f["tk"], f["mk"])
             C.quant_rows_e4m3(self.crsk, f["crsk8"], f["cscale"], f["tc"], f["mc"])
             self.key8 = self.key
@@ -248,10 +249,33 @@ class WeightMirror:
         return (self.space.version, self.space.param_flat._version,
                 sum(map(_VERSION, self._tracked)))
 
-    def _pack_t(self) -> None:
+    def _pack_t(self, side: bool = False) -> None:
         from ..ops._ext import native
-        if self.ntensors:
+        if not self.ntensors:
+            return
+        self._join_pack()  # a previous side-stream pack must be done before krsc changes again
+        s = None
+        # (not under graph capture: the fork would stay unjoined at the end of the captured step)
+        if side and self.krsc.is_cuda and not torch.cuda.is_current_stream_capturing():
+            from ..ops import streams
+            s = streams.wgrad_stream(self.krsc.device)
+        if s is None:
             native().pack_t_batched(self.krsc, self.crsk, self.table, self.max_tiles)
+            return
+        # the dgrad layout is first read in backward: build it beside the forward (side stream),
+        # and make the first consumer's stream wait for it (crsk_view)
+        s.wait_stream(torch.cuda.current_stream(self.krsc.device))
+        with torch.cuda.stream(s):
+            native().pack_t_batched(self.krsc, self.crsk, self.table, self.max_tiles)
+            ev = torch.cuda.Event()
+            ev.record(s)
+        self._crsk_event = ev
+
+    def _join_pack(self) -> None:
+        ev = getattr(self, "_crsk_event", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.krsc.device).wait_event(ev)
+            self._crsk_event = None
 
     def refresh(self) -> None:
         from ..ops._ext import native
@@ -266,7 +290,7 @@ class WeightMirror:
     def after_optimizer_step(self) -> None:
         """The fused SGD step just wrote ``krsc``; rebuild ``crsk`` and mark both current."""
         self.space.version += 1
-        self._pack_t()
+        self._pack_t(side=True)
         self.key = self.current_key()
 
     def valid(self) -> bool:
@@ -276,7 +300,10 @@ class WeightMirror:
         return self._krsc_views.get(id(p)) if self.valid() else None
 
     def crsk_view(self, p) -> Optional[torch.Tensor]:
-        return self._crsk_views.get(id(p)) if self.valid() else None
+        if not self.valid():
+            return None
+        self._join_pack()
+        return self._crsk_views.get(id(p))
 
 
 def flatten_buffers(module: torch.nn.Module) -> Dict[torch.dtype, torch.Tensor]:

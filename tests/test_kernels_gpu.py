@@ -928,3 +928,35 @@ def test_stem_bwd_fused_matches_unfused(gpu, native_ext, n, h, w, det):
     ref_e = C.stem_wgrad(dy_e, xsp, [64, 3, 7, 7], det)
     got_e = C.stem_bwd_fused(dpool, idx, y, stats, gamma, sums, False, xsp, [64, 3, 7, 7], det)
     assert _rel_err(got_e, ref_e) < 1e-3
+
+
+@pytest.mark.parametrize("n,h,w", [(4, 112, 112), (3, 57, 45)])  # odd sizes: clipped edge windows
+def test_stem_pool_argmax_y_reduction(gpu, native_ext, n, h, w):
+    """The stem's BN backward reduction from the pooled tensors: bn_relu_maxpool(argmax_y=True)
+    also returns u = y at every window's argmax (bitwise a copy of y's element), and the plain
+    streaming reduction bn_act_bwd_reduce(dpool, -, u, mask=2) equals the gather over y
+    (pool_bn_bwd_reduce) up to fp32 summation order."""
+    C = native_ext
+    torch.manual_seed(5)
+    y = torch.randn(n, h, w, 64, device=gpu).bfloat16()
+    scale = torch.randn(64, device=gpu)
+    shift = torch.randn(64, device=gpu) * 0.3
+    mean = torch.randn(64, device=gpu) * 0.1
+    stats = torch.stack([mean, torch.rand(64, device=gpu) + 0.5, scale, shift]).contiguous()
+    out, idx = C.bn_relu_maxpool(y, scale, shift)
+    out2, idx2, u = C.bn_relu_maxpool(y, scale, shift, True)
+    assert torch.equal(out, out2) and torch.equal(idx, idx2)
+    ho, wo = out.shape[1], out.shape[2]
+    k = idx.long()
+    ii = torch.arange(ho, device=gpu).view(1, ho, 1, 1)
+    jj = torch.arange(wo, device=gpu).view(1, 1, wo, 1)
+    hh = (2 * ii - 1 + k // 3).clamp(0, h - 1)
+    ww = (2 * jj - 1 + k % 3).clamp(0, w - 1)
+    nn_ = torch.arange(n, device=gpu).view(n, 1, 1, 1).expand_as(k)
+    cc = torch.arange(64, device=gpu).view(1, 1, 1, 64).expand_as(k)
+    assert torch.equal(u, y[nn_, hh, ww, cc])
+    dpool = torch.randn(out.shape, device=gpu).bfloat16()
+    ref = C.pool_bn_bwd_reduce(dpool, idx, y, stats)
+    got = C.bn_act_bwd_reduce(dpool, u, u, stats, 2)
+    torch.cuda.synchronize()
+    assert _rel_err(got, ref) < 1e-4
