@@ -50,9 +50,10 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--first-bucket-mb", type=float, default=1.0,
                    help="cap of the bucket all-reduced first (torch DDP: 1 MiB)")
-    p.add_argument("--last-bucket-mb", type=float, default=None,
+    p.add_argument("--last-bucket-mb", type=_last_mb, default="auto",
                    help="cap of the bucket all-reduced LAST (stem/layer1 gradients; its all-reduce "
-                        "is the exposed tail). Default: no cap (torch DDP layout)")
+                        "is the exposed tail): MB, 'none' (torch DDP layout) or 'auto' (default: "
+                        "the xGMI tail model's choice, parallel/buckets.py auto_last_bucket_mb)")
     p.add_argument("--force-comm", action="store_true",
                    help="native impl: run the RCCL communicator + C++ reducer + buffer broadcasts "
                         "even at N=1 (world-1 RCCL communicator; exercises the multi-GPU path)")
@@ -95,6 +96,12 @@ def _relaunch_with_torchrun(args_argv, n) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+def _last_mb(v: str):
+    if v in ("auto", "none"):
+        return None if v == "none" else v
+    return float(v)
 
 
 def main(argv=None) -> int:
@@ -268,7 +275,8 @@ def main(argv=None) -> int:
                        "bucket_mb": args.bucket_mb, "wire_dtype": args.wire_dtype, "comm_backend": args.comm,
                        "cudnn_benchmark": bool(args.cudnn_benchmark), "graph": bool(args.graph),
                        "deterministic": bool(args.deterministic), "force_comm": bool(args.force_comm),
-                       "first_bucket_mb": args.first_bucket_mb, "last_bucket_mb": args.last_bucket_mb,
+                       "first_bucket_mb": args.first_bucket_mb,
+                       "last_bucket_mb": ddp.last_bucket_mb if args.impl == "native" else args.last_bucket_mb,
                        "comm": comm, "final_loss": round(final_loss, 4)},
         }
         line = json.dumps(res)

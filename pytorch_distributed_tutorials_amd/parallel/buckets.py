@@ -113,3 +113,29 @@ def tail_time_us(plan_bytes: Sequence[int], world: int, links_used: int = 1) -> 
     if not plan_bytes:
         return 0.0
     return allreduce_us(int(plan_bytes[-1]), world, links_used)
+
+
+def auto_last_bucket_mb(param_sizes_bytes: Sequence[int], world: int, bucket_cap_mb: float = 25.0,
+                        first_bucket_mb: float = 1.0, links_used: int = XGMI_LINKS,
+                        candidates: Sequence[float] = (0.25, 0.5, 1.0, 2.0, 4.0, 8.0, 16.0)) -> Optional[float]:
+    """The last-bucket cap the tail model prefers for this model and world size (None = no cap).
+
+    The last bucket's all-reduce is the only one no backward kernel hides (``tail_time_us``), so a
+    smaller last bucket shortens the step; every extra bucket costs one more collective launch,
+    counted here at a quarter of ``RCCL_LAUNCH_US`` (it overlaps backward, but serialises on the
+    comm stream).  World 1 has no all-reduce: None."""
+    if world <= 1:
+        return None
+    base = ddp_bucket_plan(param_sizes_bytes, bucket_cap_mb, first_bucket_mb, None)
+
+    def cost(cap):
+        plan = ddp_bucket_plan(param_sizes_bytes, bucket_cap_mb, first_bucket_mb, cap)
+        nbytes = [sum(int(param_sizes_bytes[i]) for i in b) for b in plan]
+        return tail_time_us(nbytes, world, links_used) + 0.25 * RCCL_LAUNCH_US * (len(plan) - len(base))
+
+    best, best_cost = None, cost(None)
+    for cap in candidates:
+        c = cost(cap)
+        if c < best_cost - 1e-9:
+            best, best_cost = cap, c
+    return best

@@ -38,7 +38,7 @@ import torch.nn as nn
 
 from ..ops._ext import native_available
 from . import comm as pcomm
-from .buckets import ddp_bucket_plan
+from .buckets import auto_last_bucket_mb, ddp_bucket_plan
 from .flat import FlatParamSpace, flatten_buffers
 
 
@@ -141,7 +141,7 @@ class DistributedDataParallel(nn.Module):
                  bucket_cap_mb: Optional[float] = None, first_bucket_mb: float = 1.0,
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  comm: str = "auto", wire_dtype: str = "fp32", average: bool = True,
-                 last_bucket_mb: Optional[float] = None, force_reducer: bool = False,
+                 last_bucket_mb="auto", force_reducer: bool = False,
                  comm_options: Optional["pcomm.CommOptions"] = None):
         super().__init__()
         self.module = module
@@ -151,7 +151,7 @@ class DistributedDataParallel(nn.Module):
         self.process_group = process_group
         self.bucket_cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
         self.first_bucket_mb = first_bucket_mb
-        self.last_bucket_mb = last_bucket_mb
+        self.last_bucket_mb = last_bucket_mb  # "auto": the xGMI tail model picks it (below)
         self.find_unused_parameters = find_unused_parameters  # unused params are zero-filled
         self.average = average
         if wire_dtype not in ("fp32", "bf16"):
@@ -178,6 +178,13 @@ class DistributedDataParallel(nn.Module):
 
         # ---- flat layout in bucket order
         sizes = [p.numel() * p.element_size() for p in params]
+        if isinstance(self.last_bucket_mb, str):
+            if self.last_bucket_mb != "auto":
+                raise ValueError(f"last_bucket_mb must be a number, None or 'auto', got {self.last_bucket_mb!r}")
+            # the last bucket's all-reduce is the one nothing hides: cap it where the tail model
+            # says the step is shortest (None at world 1: no all-reduce to hide)
+            self.last_bucket_mb = auto_last_bucket_mb(sizes, self.world_size, self.bucket_cap_mb,
+                                                      self.first_bucket_mb)
         plan = ddp_bucket_plan(sizes, self.bucket_cap_mb, self.first_bucket_mb, self.last_bucket_mb)
         layout = [i for b in plan for i in b]
         self.comm_options = comm_options or pcomm.CommOptions.from_env()

@@ -293,3 +293,20 @@ def test_sgd_flat_space_check_cache_tracks_the_param_list():
     assert opt._flat_space_of(g) is sp
     assert set(opt.state_dict()["param_groups"][0]) == set(g) - {"params"} | {"params"}
     assert not any(k.startswith("_pdt") for k in opt.state_dict()["param_groups"][0])
+
+
+def test_auto_last_bucket_cap_from_tail_model():
+    # DDP's default last_bucket_mb="auto": the tail model caps the last-launched bucket (stem and
+    # early layer1 gradients, produced at the very end of backward) so its exposed all-reduce
+    # shrinks; at world 1 there is no all-reduce and the torch layout is kept
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.parallel.buckets import auto_last_bucket_mb, tail_time_us
+    sizes = [p.numel() * 4 for p in build_model("resnet50", num_classes=1000).parameters()]
+    assert auto_last_bucket_mb(sizes, 1) is None
+    for world in (2, 8):
+        cap = auto_last_bucket_mb(sizes, world)
+        assert cap is not None and cap <= 2.0
+        base = [sum(sizes[i] for i in b) for b in ddp_bucket_plan(sizes)]
+        capped = [sum(sizes[i] for i in b) for b in ddp_bucket_plan(sizes, last_bucket_mb=cap)]
+        assert capped[-1] <= cap * 2**20 and sum(capped) == sum(base)
+        assert tail_time_us(capped, world, 7) < tail_time_us(base, world, 7)
