@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import operator
 import os
+import weakref
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -27,6 +28,18 @@ def _is_dense(t: torch.Tensor) -> bool:
 
 
 _VERSION = operator.attrgetter("_version")
+# mirrors with a side-stream pack whose event no stream has waited on yet
+_PENDING_PACKS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def forget_completed_side_packs() -> None:
+    """Drop the pending side-stream pack events of every mirror.  Only valid right after a device
+    synchronize (the packs are done): a graph capture calls it before it starts, because waiting on
+    an event recorded by eager work from inside a capture is a HIP error
+    (hipErrorStreamCaptureIsolation)."""
+    for m in list(_PENDING_PACKS):
+        m._crsk_event = None
+    _PENDING_PACKS.clear()
 
 
 class FlatParamSpace:
@@ -270,12 +283,14 @@ class WeightMirror:
             ev = torch.cuda.Event()
             ev.record(s)
         self._crsk_event = ev
+        _PENDING_PACKS.add(self)
 
     def _join_pack(self) -> None:
         ev = getattr(self, "_crsk_event", None)
         if ev is not None:
             torch.cuda.current_stream(self.krsc.device).wait_event(ev)
             self._crsk_event = None
+            _PENDING_PACKS.discard(self)
 
     def refresh(self) -> None:
         from ..ops._ext import native

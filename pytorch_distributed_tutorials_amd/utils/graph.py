@@ -17,6 +17,7 @@ the ResNet graph is static (same shapes, same buckets, every step).
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, List, Optional, Tuple
 
 import torch
@@ -81,12 +82,37 @@ class CapturedStep:
                 probe = self.step_fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # side-stream work the warm-up left pending (weight-layout packs) is done now; the capture
+        # must not wait on its events (recorded outside the capture)
+        from ..parallel.flat import forget_completed_side_packs
+        forget_completed_side_packs()
         # output buffers: allocated here, before any capture, so they live outside the pool
         if probe is not None:
             self.outputs = [torch.empty_like(probe) for _ in range(self.period)]
         else:  # no eager warm-up: the step returns its loss, an fp32 scalar
             self.outputs = [torch.empty((), dtype=torch.float32, device=torch.cuda.current_device()) for _ in range(self.period)]
+        # no cyclic garbage collection while capturing: a collected cycle that owns a HIP event or
+        # graph (autograd contexts of earlier steps) would be destroyed inside the capture, which
+        # aborts the process; collect before (and before the ring snapshot, whose entries belong to
+        # live objects), and let anything created during capture wait
+        gc.collect()
         start = self.ring[0]() if self.ring is not None else ()
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            self._capture_graphs()
+        finally:
+            if gc_was_on:
+                gc.enable()
+        if self.ring is not None:
+            end = self.ring[0]()
+            if len(end) != len(start):
+                raise RuntimeError("CapturedStep: the captured step created new ring state; warm it up first")
+            self.delta = tuple((e - b) // self.period for b, e in zip(start, end))
+            self.ring[1](start)  # the device has run none of the captured steps yet
+        torch.cuda.synchronize()
+
+    def _capture_graphs(self) -> None:
         pool = self.pool
         for k in range(self.period):
             if self.ring is not None:
@@ -102,13 +128,6 @@ class CapturedStep:
             if pool is None:
                 pool = g.pool()  # later phases reuse the first graph's private pool
             self.graphs.append(g)
-        if self.ring is not None:
-            end = self.ring[0]()
-            if len(end) != len(start):
-                raise RuntimeError("CapturedStep: the captured step created new ring state; warm it up first")
-            self.delta = tuple((e - b) // self.period for b, e in zip(start, end))
-            self.ring[1](start)  # the device has run none of the captured steps yet
-        torch.cuda.synchronize()
 
     def in_phase(self) -> bool:
         """False when eager work moved the host counters off the next replay's baked-in phase."""
