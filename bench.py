@@ -240,6 +240,16 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.item())
+    # host issue cost of one step from an idle device (untimed, after the timed region): the time
+    # inside step() above also counts waits on a full launch queue whenever the GPU is the bound
+    issue = []
+    for _ in range(3):
+        barrier()
+        th = time.perf_counter()
+        step()
+        issue.append(time.perf_counter() - th)
+    barrier()
+    host_issue_ms = 1000.0 * min(issue)
     comm = None
     if args.impl == "native":
         info = ddp.bucket_info()
@@ -262,6 +272,7 @@ def main(argv=None) -> int:
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "host_ms_per_step": round(1000.0 * host / args.steps, 3),
+            "host_issue_ms": round(host_issue_ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(img_s / base, 4) if base else None),

@@ -1256,6 +1256,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("fmt_a") = 0, py::arg("fmt_b") = 0, py::arg("scale_a") = 127, py::arg("scale_b") = 127,
         py::arg("use_scale") = true);
   m.def("conv_nt_group_rows", &pdt::conv_nt_group_rows, py::arg("M"), py::arg("Nout"), py::arg("kg_bytes"));
+  m.def("nt_timing_fetch", [](int n) {
+    // PDT_NT_TIMING variant builds: [n] per-block phase timestamps of NT launches (else empty)
+    auto out = torch::zeros({n}, torch::dtype(torch::kInt64));
+    const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
+    return out.narrow(0, 0, got);
+  }, py::arg("n"));
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);

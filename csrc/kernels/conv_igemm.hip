@@ -152,6 +152,36 @@ constexpr int EPI_PLAIN = 0;  // store (+ optional addend)
 constexpr int EPI_STATS = 1;  // + BN forward partial statistics (conv fwd)
 constexpr int EPI_BNB = 2;    // + fused BN backward relu-mask and partial sums (conv dgrad)
 
+#ifdef PDT_NT_TIMING
+constexpr int kNtTimingSlots = 8 * 65536;
+__device__ unsigned long long g_nt_timing[kNtTimingSlots];
+#define NT_STAMP(i)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {                                        \
+      g_nt_timing[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();                   \
+      if ((i) == 0) {                                                                    \
+        g_nt_timing[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();               \
+        g_nt_timing[blockIdx.x * 8 + 7] = (unsigned long long)__smid();                   \
+      }                                                                                  \
+    }                                                                                    \
+  } while (0)
+#else
+#define NT_STAMP(i) do {} while (0)
+#endif
+
+int nt_timing_fetch(unsigned long long* host, int n) {
+#ifdef PDT_NT_TIMING
+  n = std::min(n, kNtTimingSlots);
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nt_timing), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return n;
+#else
+  (void)host; (void)n;
+  return 0;
+#endif
+}
+
+
 // LDS image of a [rows][64] bf16 tile: 128-B rows, 16-B chunk XOR-swizzled by (row>>1)&7.
 // For the 16x16x32 fragment read (lane l: row l&15, chunk 4*ksub + (l>>4)) every ds_read_b128
 // lane group then touches 16 distinct 16-B slots of the 256-B bank row: conflict-free.
@@ -258,6 +288,17 @@ constexpr int nt_min_waves() {
 // statistics (EPI_STATS) or the fused BN-backward mask / partial sums (EPI_BNB), bf16 staging
 // through LDS (`smem`, idle pipeline buffers: every wave must be past its last fragment read)
 // and 16-byte row stores.  Every thread of the workgroup calls it (it has block barriers).
+// EPI_STATS: where the BN statistics are summed.  1 (default): in the store loop, from the bf16
+// chunks each lane stores -- the lane's 8 channels are fixed, so a chunk costs 8 unpacks + 4
+// v_pk_add_f32 + 4 v_pk_fma_f32, and one shuffle reduction over the lanes sharing the channels
+// follows.  0: from the fp32 accumulators before staging (one 16-lane DPP row reduction per
+// channel value: ~600 VALU + hazard nops per wave on the 256x256 tile, measured 7.9k cycles per
+// tile with the PDT_NT_TIMING build -- as long as the main loop of a short-K 1x1 conv).  The
+// bf16 statistics are those of the tensor the BN apply reads (torch's autocast semantics).
+#ifndef PDT_STATS_STORE
+#define PDT_STATS_STORE 1
+#endif
+
 template <class CFG, int WM, int WN, int TM, int TN, int EPI, int OP>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN], char* smem, int m0, int n0,
                                             int tmi) {
@@ -287,7 +328,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
     }
   }
 
-  if constexpr (EPI == EPI_STATS) {
+  if constexpr (EPI == EPI_STATS && !PDT_STATS_STORE) {
     // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels,
     // converted to M2 about the wave's mean (cancellation is benign at <= 64 rows).  The WM wave
     // rows of the workgroup are then merged in LDS (Chan: M2 = sum M2_w + sum n_w (mean_w -
@@ -360,6 +401,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
     __syncthreads();  // red[] aliases the staging rows written next
   }
 
+  NT_STAMP(3);
   // stage the wave's pixels x channels tile as bf16 (8-byte writes), then 16-byte row stores
   char* ep = smem + wid * (TM * 16) * CFG::EPI_PITCH;
 #pragma unroll
@@ -378,6 +420,9 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   static_assert(64 % CH_PER_ROW == 0, "a lane keeps one channel chunk across the store loop");
   // EPI_BNB: this lane's 8 channels are fixed (c = lane % CH_PER_ROW); per-lane partial sums
   float bmu[8], bsc[8], bsh[8], bsg[8], bsq[8];
+  pdt_f2 st_s[4], st_q[4];  // EPI_STATS (store-loop form): the lane's 8 channels, as pairs
+#pragma unroll
+  for (int h = 0; h < 4; ++h) { st_s[h] = pdt_f2{0.f, 0.f}; st_q[h] = pdt_f2{0.f, 0.f}; }
   if constexpr (EPI == EPI_BNB) {
     const int colb = min(wcol0 + (lane % CH_PER_ROW) * 8, P.Nout - 8);
 #pragma unroll
@@ -532,6 +577,16 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
             bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
           }
         }
+        if constexpr (EPI == EPI_STATS && PDT_STATS_STORE) {
+          // rows past the GEMM edge were staged as 0 (their accumulators are 0): no mask needed
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t w = (uint32_t)v[h];
+            const pdt_f2 a2 = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+            st_s[h] += a2;
+            st_q[h] = __builtin_elementwise_fma(a2, a2, st_q[h]);
+          }
+        }
         if (ooff[it] != OOB) *reinterpret_cast<v4i*>(reinterpret_cast<char*>(P.out) + ooff[it]) = v;
       }
     }
@@ -557,6 +612,62 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
     }
   } else {
     if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{});
+  }
+  if constexpr (EPI == EPI_STATS && PDT_STATS_STORE) {
+    float s8[8], q8[8];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) { s8[2 * h] = st_s[h].x; s8[2 * h + 1] = st_s[h].y; q8[2 * h] = st_q[h].x; q8[2 * h + 1] = st_q[h].y; }
+    // lanes holding the same channel chunk (lane, lane + CH_PER_ROW, ...) -> the wave's TM*16 rows
+#pragma unroll
+    for (int o = CH_PER_ROW; o < 64; o <<= 1)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        s8[q] += __shfl_xor(s8[q], o, 64);
+        q8[q] += __shfl_xor(q8[q], o, 64);
+      }
+    // M2 about the wave's mean (cancellation benign at <= 64 rows), then the WM wave rows of the
+    // workgroup merge in LDS (Chan) into ONE partial per (row tile, channel), as bn_finalize reads
+    const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
+    const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
+    __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
+    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    if (lane < CH_PER_ROW) {
+      float m2[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m2[q] = fmaxf(q8[q] - s8[q] * s8[q] * inv_valid, 0.f);
+      float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
+      *reinterpret_cast<float4*>(rp) = make_float4(s8[0], s8[1], s8[2], s8[3]);
+      *reinterpret_cast<float4*>(rp + 4) = make_float4(s8[4], s8[5], s8[6], s8[7]);
+      *reinterpret_cast<float4*>(rp + BN) = make_float4(m2[0], m2[1], m2[2], m2[3]);
+      *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(m2[4], m2[5], m2[6], m2[7]);
+    }
+    __syncthreads();
+    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
+      float sw[WM], qw[WM], nw[WM];
+      float S = 0.f, Nr = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        nw[w] = (float)max(0, min(TM * 16, P.M - (m0 + w * TM * 16)));
+        sw[w] = red[(w * 2 + 0) * BN + t];
+        qw[w] = red[(w * 2 + 1) * BN + t];
+        S += sw[w];
+        Nr += nw[w];
+      }
+      const float mean = S / Nr;  // Nr > 0: the tile's first wave row is inside the GEMM
+      float Q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        if (nw[w] > 0.f) {
+          const float d = sw[w] / nw[w] - mean;
+          Q += qw[w] + nw[w] * d * d;
+        }
+      }
+      const int col = n0 + t;
+      if (col < P.Nout) {
+        P.part[((int64_t)tmi * 2 + 0) * P.Nout + col] = S;
+        P.part[((int64_t)tmi * 2 + 1) * P.Nout + col] = Q;
+      }
+    }
   }
   if constexpr (EPI == EPI_BNB) {
     // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
@@ -617,6 +728,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
   const int m0 = tmi * BM, n0 = tni * BN;
 
+  NT_STAMP(0);
   const int t = threadIdx.x;
   // wave id through readfirstlane: uniform for the compiler, so every LDS-DMA destination
   // (tile base + wave slot) is scalar math + one m0 write, no VGPR add + readfirstlane per load
@@ -904,6 +1016,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
     if (p < nk) issue(p, p);
   wait_steps<LPS>(min(nk, STAGES - 1) - 1);
   lds_barrier();
+  NT_STAMP(1);
   int cur = 0, nxt = STAGES - 1;
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, nxt);
@@ -955,7 +1068,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   }  // !HALO
 
   // --------------------------------------------------------------- epilogue
+  NT_STAMP(2);
   nt_epilogue<CFG, WM, WN, TM, TN, EPI, OP>(P, acc, smem, m0, n0, tmi);
+  NT_STAMP(4);
 }
 
 

@@ -67,6 +67,10 @@ struct ConvShape {
 int conv_nt_group_rows(int M, int Nout, int kg_bytes);
 // (BM, BN) of the NT workgroup tile the fwd / dgrad launch of such a GEMM runs (test introspection)
 void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn);
+// PDT_NT_TIMING builds (scripts/build_variant.sh): per-workgroup phase timestamps of NT launches
+// (s_memtime at start / first operands in LDS / main loop done / epilogue stats done / end, plus
+// s_memrealtime and the CU id), 8 values per block id, copied into `host`; other builds return 0.
+int nt_timing_fetch(unsigned long long* host, int n);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
                      const ConvShape& s, hipStream_t st);
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="also time the fp8 (e4m3) forward conv")
     ap.add_argument("--bn", action="store_true", help="also time dgrad with the fused BN-backward epilogue")
     ap.add_argument("--det", action="store_true", help="wgrad in deterministic mode (split-K slabs + reduce)")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="which products to time (others report 0)")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda:0")
@@ -94,12 +95,14 @@ def main():
         wk = C.pack_weight(wt, cx)
         dy = torch.randn(N, ho, wo, k, device=dev).to(torch.bfloat16)
         flop = 2.0 * N * ho * wo * k * c * r * s
-        f = timeit(lambda: C.conv_fwd(x, wk, st, pd, True), a.iters)
-        d = timeit(lambda: C.conv_dgrad(dy, wt, [N, h, w, c], st, pd), a.iters) if c % 8 == 0 else 0.0
-        g = timeit(lambda: C.conv_wgrad(dy, x, [k, c, r, s], st, pd, a.det), a.iters)
+        ops = a.ops.split(",")
+        f = timeit(lambda: C.conv_fwd(x, wk, st, pd, True), a.iters) if "fwd" in ops else 0.0
+        d = timeit(lambda: C.conv_dgrad(dy, wt, [N, h, w, c], st, pd), a.iters) \
+            if c % 8 == 0 and "dgrad" in ops else 0.0
+        g = timeit(lambda: C.conv_wgrad(dy, x, [k, c, r, s], st, pd, a.det), a.iters) if "wgrad" in ops else 0.0
         row = [c, h, w, k, r, s, st, pd, cnt, N * ho * wo, k, c * r * s,
-               round(f, 3), round(flop / f / 1e9, 1), round(d, 3), round(flop / d / 1e9, 1) if d else 0,
-               round(g, 3), round(flop / g / 1e9, 1)]
+               round(f, 3), round(flop / f / 1e9, 1) if f else 0, round(d, 3), round(flop / d / 1e9, 1) if d else 0,
+               round(g, 3), round(flop / g / 1e9, 1) if g else 0]
         tot["fwd"] += f * cnt
         tot["dgrad"] += d * cnt
         tot["wgrad"] += g * cnt
@@ -144,7 +147,7 @@ def main():
     summ = {k: round(v, 3) for k, v in tot.items() if k != "flop"}
     allms = tot["fwd"] + tot["dgrad"] + tot["wgrad"]
     summ["native_total_ms"] = round(allms, 3)
-    summ["native_TFLOPs"] = round(3 * tot["flop"] / allms / 1e9, 1)
+    summ["native_TFLOPs"] = round(3 * tot["flop"] / allms / 1e9, 1) if allms else 0
     print(json.dumps(summ))
     if a.json:
         with open(a.json, "w") as fh:
