@@ -1550,13 +1550,37 @@ static bool use_wide_tile(int M, int Nout, int kg_bytes) {
   return kg_bytes >= 256 && blocks >= 196;
 }
 
+// Short-K GEMMs with Nout % 256 == 0 (the 1x1 convs' K <= PDT_NT_MID elements): a 4-wave 128x256
+// tile (waves of 64x128, the 256x256 tile's wave shape) on the K32 ring, so its LDS (72 KB) lets
+// TWO blocks share a CU: one block's epilogue stores overlap the other's loads and MFMAs.  The
+// 8-wave 256x256 tile holds a CU alone, and its phases (load, MFMA, store) run back to back:
+// PDT_NT_TIMING measured ~45 % of a 256x256 short-K tile in the store phase while HBM idles in
+// the load/MFMA phases.  Measured on MI355X (r3j, one box, batch 256): ResNet-50 step 19.24 ms
+// (off) -> 18.94 (K <= 512) / 18.95 (K <= 256) / 19.06 (K <= 1024); isolated fwd 4.22 -> 4.16 ms,
+// BN-fused dgrad 5.65 -> 5.52 ms.  0 disables it.
+static int nt_mid_kmax() {
+  static int v = -1;
+  if (v < 0) {
+    v = 512;
+    if (const char* e = getenv("PDT_NT_MID")) v = std::max(0, atoi(e));
+  }
+  return v;
+}
+
+static bool use_mid_tile(int M, int Nout, int kg_bytes) {
+  const int kmax = nt_mid_kmax();
+  return kmax > 0 && M > 8192 && Nout % 256 == 0 && kg_bytes <= 2 * kmax;
+}
+
 // Tile choice: output channels 64 -> tall 256x64 tile (more M rows per block); small M -> short
-// 64x128 tile; big GEMMs -> 256x256, else 128x128.  Returns the tile's BM, which is also the row
+// 64x128 tile; short-K with Nout % 256 == 0 -> 128x256 (use_mid_tile); big GEMMs -> 256x256, else
+// 128x128.  Returns the tile's BM, which is also the row
 // group of the BN partials the STATS / BNB epilogues write (one per workgroup row tile): hosts
 // size those buffers with it, dispatch_nt picks its tile with it -- one definition for both.
 int conv_nt_group_rows(int M, int Nout, int kg_bytes) {
   if (Nout <= 64) return 256;
   if (M <= 8192) return 64;
+  if (use_mid_tile(M, Nout, kg_bytes)) return 128;
   return use_wide_tile(M, Nout, kg_bytes) ? 256 : 128;
 }
 
@@ -1567,6 +1591,7 @@ void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn) {
   if (Nout <= 64) { *bm = 256; *bn = 64; }
   else if (rows == 64) { *bm = 64; *bn = 128; }
   else if (rows == 256) { *bm = 256; *bn = 256; }
+  else if (use_mid_tile(M, Nout, kg_bytes)) { *bm = 128; *bn = 256; }
   else { *bm = 128; *bn = 128; }
 }
 
@@ -1599,6 +1624,8 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
   } else if (rows == 256) {
     if (k32ok && nt_k32(2, a, EPI)) run_nt<4, 2, 4, 8, 5, C64, EPI, OP_BF16, true>(a, st);  // 256 x 256
     else run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);
+  } else if (k32ok && use_mid_tile(a.M, a.Nout, a.Kg * 2)) {
+    run_nt<2, 2, 4, 8, 3, C64, EPI, OP_BF16, true>(a, st);  // 128 x 256, K32 ring, 2 blocks / CU
   } else {
     if (k32ok && nt_k32(3, a, EPI)) run_nt<2, 2, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 128 x 128
     else run_nt<2, 2, 4, 4, 2, C64, EPI>(a, st);

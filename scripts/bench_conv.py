@@ -95,7 +95,7 @@ def main():
         wk = C.pack_weight(wt, cx)
         dy = torch.randn(N, ho, wo, k, device=dev).to(torch.bfloat16)
         flop = 2.0 * N * ho * wo * k * c * r * s
-        ops = a.ops.split(",")
+        ops = a.ops.replace("+", ",").split(",")
         f = timeit(lambda: C.conv_fwd(x, wk, st, pd, True), a.iters) if "fwd" in ops else 0.0
         d = timeit(lambda: C.conv_dgrad(dy, wt, [N, h, w, c], st, pd), a.iters) \
             if c % 8 == 0 and "dgrad" in ops else 0.0

@@ -8,7 +8,7 @@ kernel with an fp32 reference of the same op:
 
 * bf16 forward + BN partial statistics, plain dgrad, BN-fused dgrad in every ReLU-mask mode
   (0 none, 1 z > 0, 2 recomputed from y, 3 bitmask) with and without the residual-gradient
-  addend, on the 256x256 / 128x128 / 256x64 / 64x128 tiles;
+  addend, on the 256x256 / 128x256 / 128x128 / 256x64 / 64x128 tiles;
 * fp8 forward and dgrad on the 256x256 tile;
 * the whole ResNet-50 (224 px family at 112 px, batch 32) against the fp32 stock model with
   identical weights;
@@ -49,9 +49,10 @@ def _operands(shape, dev, seed):
 
 # forward GEMM: M = N*Ho*Wo, Nout = K, K_gemm = R*S*C
 FWD_TILES = [
-    ((16, 56, 56, 128, 256, 1, 1, 1, 0), (256, 256)),   # layer1->2 style 1x1, 196 row tiles
+    ((16, 56, 56, 128, 256, 1, 1, 1, 0), (128, 256)),   # short-K 1x1, Nout % 256 == 0: 2 blocks / CU
+    ((16, 56, 56, 1024, 256, 1, 1, 1, 0), (256, 256)),  # long-K 1x1, 196 row tiles
     ((64, 28, 28, 128, 256, 3, 3, 1, 1), (256, 256)),   # 3x3 on the wide tile
-    ((4, 56, 56, 64, 256, 1, 1, 1, 0), (128, 128)),
+    ((4, 56, 56, 64, 128, 1, 1, 1, 0), (128, 128)),
     ((8, 32, 32, 64, 64, 3, 3, 1, 1), (256, 64)),
     ((2, 14, 14, 256, 256, 3, 3, 1, 1), (64, 128)),
 ]
@@ -78,10 +79,12 @@ def test_fwd_stats_per_tile(gpu, native_ext, shape, tile):
 
 # dgrad GEMM (per parity class): M = N*H*W / stride^2, Nout = C, K_gemm = R*S*K
 DGRAD_TILES = [
-    ((16, 56, 56, 256, 128, 1, 1, 1, 0), (256, 256)),
+    ((16, 56, 56, 256, 128, 1, 1, 1, 0), (128, 256)),   # short-K (K = 128): the 128x256 tile
+    ((16, 56, 56, 256, 1024, 1, 1, 1, 0), (256, 256)),  # long-K 1x1 on the wide tile
     ((64, 28, 28, 256, 128, 3, 3, 1, 1), (256, 256)),
-    ((64, 56, 56, 256, 512, 1, 1, 2, 0), (256, 256)),   # stride-2 parity classes on the wide tile
-    ((4, 56, 56, 256, 64, 1, 1, 1, 0), (128, 128)),
+    ((64, 56, 56, 256, 512, 1, 1, 2, 0), (128, 256)),   # stride-2 parity classes, short K
+    ((64, 56, 56, 256, 1024, 1, 1, 2, 0), (256, 256)),  # stride-2 parity classes on the wide tile
+    ((4, 56, 56, 128, 64, 1, 1, 1, 0), (128, 128)),
     ((8, 32, 32, 64, 64, 3, 3, 1, 1), (256, 64)),
     ((2, 14, 14, 256, 256, 3, 3, 1, 1), (64, 128)),
 ]
@@ -156,10 +159,10 @@ def _deq(q, fmt):
 def test_fp8_fwd_and_dgrad_on_wide_tile(gpu, native_ext):
     from pytorch_distributed_tutorials_amd.ops.fused import _packed_crsk8
     C = native_ext
-    shape = (16, 56, 56, 256, 256, 1, 1, 1, 0)
+    shape = (16, 56, 56, 256, 256, 3, 3, 1, 1)   # long K: short-K 1x1s leave the wide tile
     n, h, w, c, k, r, s, st, pd = shape
-    assert tuple(C.conv_nt_tile(n * h * w, k, c)) == (256, 256)      # fwd: K_gemm bytes = C
-    assert tuple(C.conv_nt_tile(n * h * w, c, k)) == (256, 256)      # dgrad: K_gemm bytes = K
+    assert tuple(C.conv_nt_tile(n * h * w, k, r * s * c)) == (256, 256)  # fwd: K_gemm bytes = 9C
+    assert tuple(C.conv_nt_tile(n * h * w, c, r * s * k)) == (256, 256)  # dgrad: K_gemm bytes = 9K
     x, wt, dy = _operands(shape, gpu, 5)
     x = torch.relu(x.float()).to(torch.bfloat16)
     state = torch.zeros(C.fp8_state_floats(), device=gpu)
@@ -354,8 +357,8 @@ def test_k32_ring_bitwise_equals_k64_double_buffer(gpu, tmp_path):
     the K64 double buffer (two K=32 MFMAs per 64-deep step), so forced-K32 and forced-K64 runs of
     every tile must agree bit for bit -- outputs, BN partials and BN-backward sums."""
     res = {}
-    for mode in ("0", "1"):
-        env = dict(os.environ, PDT_NT_K32=mode)
+    for mode, env_add in (("0", {"PDT_NT_K32": "0"}), ("1", {"PDT_NT_K32": "1"}), ("mid0", {"PDT_NT_MID": "0"})):
+        env = dict(os.environ, **env_add)
         f = str(tmp_path / f"k32_{mode}.pt")
         r = subprocess.run([sys.executable, "-c", _K32_SCRIPT, ROOT, f], env=env, capture_output=True,
                            text=True, timeout=110)
@@ -364,6 +367,13 @@ def test_k32_ring_bitwise_equals_k64_double_buffer(gpu, tmp_path):
     for key, a in res["0"].items():
         for j, (u, v) in enumerate(zip(a, res["1"][key])):
             assert torch.equal(u, v), (key, j)
+    # the 128x256 short-K tile (default policy) against the 256x256 / 128x128 tiles the same GEMMs
+    # take with it disabled: same K order, so the conv outputs agree bit for bit (the BN partials
+    # are grouped by each tile's row count, so only the tensors are compared)
+    for key, a in res["0"].items():
+        b = res["mid0"][key]
+        for j in ((0,) if key.startswith("fwd") else (0, 1)):
+            assert torch.equal(a[j], b[j]), (key, j, "mid tile")
 
 
 def test_bn_reductions_concurrent_on_two_streams(gpu, native_ext):
