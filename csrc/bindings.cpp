@@ -407,6 +407,64 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
   return r;
 }
 
+// fp8 weight gradient (conv_igemm.hip igemm_tn_f8_kernel): dy8 e5m2 [N,Ho,Wo,K] and x8 e4m3 [N,H,W,C]
+// with their dequantization factors (device fp32 scalars).  Accumulates into `out` (a KRSC-dense fp32
+// view, e.g. the flat gradient buffer) or returns a fresh [K,C,R,S] channels_last tensor.  side != 0:
+// issued on that stream after the current stream's queued work, like conv_wgrad_side.
+Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const Tensor& dy_deq, const Tensor& x_deq,
+                      std::vector<int64_t> ws, int64_t stride, int64_t pad, const std::optional<Tensor>& out) {
+  TORCH_CHECK(dy8.is_cuda() && x8.is_cuda() && dy8.scalar_type() == at::kByte && x8.scalar_type() == at::kByte &&
+              dy8.dim() == 4 && x8.dim() == 4 && dy8.is_contiguous() && x8.is_contiguous(),
+              "conv_wgrad_fp8: dy8 / x8 must be contiguous uint8 NHWC device tensors");
+  TORCH_CHECK(dy_deq.is_cuda() && x_deq.is_cuda() && dy_deq.scalar_type() == at::kFloat &&
+              x_deq.scalar_type() == at::kFloat && dy_deq.numel() >= 1 && x_deq.numel() >= 1,
+              "conv_wgrad_fp8: dequantization factors must be device fp32 scalars");
+  TORCH_CHECK(ws.size() == 4, "weight shape must be [K,C,R,S]");
+  c10::hip::HIPGuard g(x8.get_device());
+  const int K = ws[0], C = ws[1], R = ws[2], S = ws[3];
+  TORCH_CHECK(x8.size(3) == C && C % 16 == 0 && K % 64 == 0, "conv_wgrad_fp8: needs C % 16 == 0, K % 64 == 0");
+  auto s = shape_of(x8.size(0), x8.size(1), x8.size(2), C, K, R, S, stride, pad);
+  TORCH_CHECK(s.Ho == dy8.size(1) && s.Wo == dy8.size(2) && K == dy8.size(3) && s.N == dy8.size(0),
+              "conv_wgrad_fp8: dy shape mismatch");
+  const auto dev = (c10::DeviceIndex)x8.get_device();
+  hipStream_t st = cur_stream(x8);
+  std::optional<c10::hip::HIPStreamGuard> sg;
+  if (side != 0) {
+    static thread_local std::unordered_map<int, hipEvent_t> evs;
+    hipEvent_t& ev = evs[(int)dev];
+    if (ev == nullptr)
+      TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+    auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
+    TORCH_CHECK(hipEventRecord(ev, st) == hipSuccess, "hipEventRecord failed");
+    TORCH_CHECK(hipStreamWaitEvent(sst.stream(), ev, 0) == hipSuccess, "hipStreamWaitEvent failed");
+    sg.emplace(sst);
+    st = sst.stream();
+  }
+  Tensor r;
+  if (out.has_value() && out->defined()) {
+    const Tensor& o = *out;
+    TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
+                o.size(2) == R && o.size(3) == S, "wgrad out: bad shape/dtype");
+    const int64_t want[4] = {(int64_t)R * S * C, 1, (int64_t)S * C, (int64_t)C};
+    for (int d = 0; d < 4; ++d)
+      TORCH_CHECK(o.size(d) == 1 || o.stride(d) == want[d], "wgrad out must be channels_last (KRSC) dense");
+    pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
+                               x_deq.data_ptr<float>(), o.data_ptr<float>(), s, true, st);
+    r = o;
+  } else {
+    auto dwp = at::empty({K, R, S, C}, x8.options().dtype(at::kFloat));
+    pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
+                               x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st);
+    r = dwp.permute({0, 3, 1, 2});
+  }
+  if (side != 0) {
+    auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
+    for (const Tensor* t : {&dy8, &x8, &dy_deq, &x_deq})
+      c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), sst);
+  }
+  return r;
+}
+
 // -------------------------------------------------------------------- stem
 // 7x7/s2 stem with C <= 4 input channels as a super-pixel conv (kernels.h): returns
 // (xsp, y, part) -- xsp is the bf16 super-pixel image (kept for the weight gradient)
@@ -1185,6 +1243,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad_side", checked("conv_wgrad_side", &conv_wgrad_side), py::arg("side"), py::arg("dy"),
         py::arg("x"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("deterministic") = false,
         py::arg("out") = py::none());
+  m.def("conv_wgrad_fp8", checked("conv_wgrad_fp8", &conv_wgrad_fp8), py::arg("side"), py::arg("dy8"),
+        py::arg("x8"), py::arg("dy_deq"), py::arg("x_deq"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"),
+        py::arg("out") = py::none());
+  m.def("conv_wgrad_fp8_plan", [](std::vector<int64_t> x_shape, std::vector<int64_t> w_shape, int stride, int pad) {
+    pdt::ConvShape s = shape_of((int)x_shape[0], (int)x_shape[1], (int)x_shape[2], (int)x_shape[3], (int)w_shape[0],
+                                (int)w_shape[2], (int)w_shape[3], stride, pad);
+    int o[4];
+    pdt::conv_wgrad_fp8_plan(s, o);
+    py::dict d;
+    d["bm"] = o[0]; d["tiles"] = o[1]; d["splits"] = o[2]; d["steps_per_split"] = o[3];
+    return d;
+  }, py::arg("x_shape"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"));
   m.def("stem_conv_fwd", checked("stem_conv_fwd", &stem_conv_fwd), py::arg("x"), py::arg("w"),
         py::arg("stride"), py::arg("pad"), py::arg("stats"));
   m.def("stem_wgrad", checked("stem_wgrad", &stem_wgrad), py::arg("dy"), py::arg("xsp"),

@@ -1395,6 +1395,211 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
     }
 }
 
+// ============================================================================
+//          TN implicit GEMM with fp8 operands (wgrad on the MX-rate MFMA)
+// ============================================================================
+// dW[Kout][R*S*C] += sum over pixels m of dy8[m][kout] (e5m2) * im2col(x8)[m][(tap, c)] (e4m3), times
+// the two operands' dequantization factors (device scalars: delayed per-tensor scaling).  A K-step
+// is 128 pixels = the K of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales), which issues
+// twice the bf16 FLOP per cycle; a K-step moves the same 128-B operand rows per pixel block as a
+// bf16 step of 64 pixels.  Both tiles sit in LDS row-major by pixel; an operand fragment is four
+// ds_read_b64_tr_b8 -- lane 2k'+h of 16-lane group g, read r: pixel row 32g + 8r + k', bytes
+// 8h..8h+7 of the fragment's 16 columns (the read transposes; profiles/r2_tr_b8_probe.md,
+// scripts/probe_f8_tn.hip).  The 16-B chunk of a row is XOR-swizzled (swz_f8) so the 8 rows of a
+// 16-lane group hit 8 distinct 4-bank groups and the two groups serviced together disjoint halves.
+// Split-K with fp32 atomics only (deterministic runs keep the bf16 slab path).
+struct TnF8Args {
+  const uint8_t* dy;   // [Mred][Kout] e5m2
+  const uint8_t* x;    // [N][H][W][C] e4m3
+  const float* dy_deq; // device scalars: real value = code * deq
+  const float* x_deq;
+  float* out;          // dW [Kout][Ncols] fp32 (atomic accumulation)
+  uint32_t dy_bytes, x_bytes;
+  int Mred, Kout, Ncols;
+  int H, W, C, S, stride, pad, stride_w;
+  FastDiv div_hw, div_w;
+  int HoWo, Wo, Ho;
+  int steps_per_split, nsteps;
+  int adv_r, adv_qh, adv_qn;  // 128 reduction rows = (adv_qn images, adv_qh output rows, adv_r columns)
+};
+
+template <int ROWB>
+__device__ __forceinline__ int swz_f8(int row) {
+  if constexpr (ROWB == 128) return (row & 7) ^ ((row >> 5) & 1);
+  else return ((row >> 2) & 1) | (((row >> 5) & 1) << 1);  // 64-B rows: 4 chunks
+}
+
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+
+template <int ROWB>
+__device__ __forceinline__ v8i frag_tr8(const char* tile, int lane, int chunk) {
+  const int g = lane >> 4, kk = (lane & 15) >> 1, h = lane & 1;
+  v8i f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 32 * g + 8 * r + kk;
+    const char* p = tile + row * ROWB + ((chunk ^ swz_f8<ROWB>(row)) << 4) + 8 * h;
+    const v2i_t v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+        (__attribute__((address_space(3))) v2i_t*)(reinterpret_cast<uintptr_t>(p)));
+    f[2 * r] = v.x;
+    f[2 * r + 1] = v.y;
+  }
+  return f;
+}
+
+template <int BMG, bool PW>
+__global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
+  constexpr int A_ROWB = BMG, B_ROWB = 128;    // bytes per pixel row of the dy / x tiles
+  constexpr int KS = 128;                      // pixels per K-step
+  constexpr int A_BYTES = KS * A_ROWB, B_BYTES = KS * B_ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int WAVES = 4;
+  constexpr int A_LPR = A_ROWB / 16, A_RPI = 64 / A_LPR;  // one 1-KiB DMA instruction: A_RPI rows
+  constexpr int A_PW = A_BYTES / 1024 / WAVES, B_PW = B_BYTES / 1024 / WAVES;
+  constexpr int TM = BMG / 32, TN = 4;         // 2 x 2 waves of (BMG/2) x 64
+  static_assert(A_PW * 1024 * WAVES == A_BYTES && B_PW * 1024 * WAVES == B_BYTES, "tile DMA split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntn = (P.Ncols + 127) / 128;
+  const int ntm = (P.Kout + BMG - 1) / BMG;
+  const int tiles = ntm * ntn;
+  const int lid = xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int split = lid / tiles;
+  const int bid = lid - split * tiles;
+  const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
+  const int k0 = tmi * BMG, c0 = tni * 128;
+  const int s_begin = split * P.steps_per_split;
+  const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
+
+  // A (dy) lanes: row within the step, source chunk (kout block of 16) that lands in LDS slot
+  int a_lane[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int arow = (wid * A_PW + i) * A_RPI + lane / A_LPR;
+    const int chk = (lane % A_LPR) ^ swz_f8<A_ROWB>(arow);
+    const int acol = k0 + chk * 16;
+    a_lane[i] = acol < P.Kout ? arow * P.Kout + acol : (int)OOB;
+  }
+  // B (x) lanes: 8 rows of 128 B per instruction; a 16-B chunk is 16 channels of one tap (C % 16 == 0)
+  int brow[B_PW], b_dh[B_PW], b_dw[B_PW], b_chb[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    brow[i] = (wid * B_PW + i) * 8 + (lane >> 3);
+    const int chk = (lane & 7) ^ swz_f8<B_ROWB>(brow[i]);
+    const int col = c0 + chk * 16;
+    const int tap = col / P.C;
+    b_chb[i] = col < P.Ncols ? col - tap * P.C : (int)OOB;
+    const int r = tap / P.S;
+    b_dh[i] = r - P.pad;
+    b_dw[i] = (tap - r * P.S) - P.pad;
+  }
+  const uint32_t WC = (uint32_t)(P.W * P.C), HWC = (uint32_t)P.H * WC;
+  uint32_t b_n[B_PW], b_ho[B_PW], b_wo[B_PW];
+  if constexpr (!PW) {
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const uint32_t m = (uint32_t)(s_begin * KS + brow[i]);
+      b_n[i] = fdiv(m, P.div_hw);
+      const uint32_t rem = m - b_n[i] * (uint32_t)P.HoWo;
+      b_ho[i] = fdiv(rem, P.div_w);
+      b_wo[i] = rem - b_ho[i] * (uint32_t)P.Wo;
+    }
+  }
+
+  auto issue = [&](int step, int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+    const int mb = step * KS;
+    const int abase = mb * P.Kout;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) glds16(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      uint32_t off;
+      if constexpr (PW) {
+        off = (uint32_t)((mb + brow[i]) * P.C + b_chb[i]);  // rows past Mred fall past the buffer
+      } else {
+        const uint32_t h = __umul24(b_ho[i], (uint32_t)P.stride) + (uint32_t)b_dh[i];
+        const uint32_t w = __umul24(b_wo[i], (uint32_t)P.stride_w) + (uint32_t)b_dw[i];
+        const bool ok = h < (uint32_t)P.H && w < (uint32_t)P.W;
+        const uint32_t o = __umul24(b_n[i], HWC) + __umul24(h, WC) + __umul24(w, (uint32_t)P.C) + (uint32_t)b_chb[i];
+        off = ok ? o : OOB;
+        uint32_t wo = b_wo[i] + (uint32_t)P.adv_r;
+        const uint32_t c1 = wo >= (uint32_t)P.Wo ? 1u : 0u;
+        b_wo[i] = c1 ? wo - (uint32_t)P.Wo : wo;
+        uint32_t ho = b_ho[i] + (uint32_t)P.adv_qh + c1;
+        const uint32_t c2 = ho >= (uint32_t)P.Ho ? 1u : 0u;
+        b_ho[i] = c2 ? ho - (uint32_t)P.Ho : ho;
+        b_n[i] += (uint32_t)P.adv_qn + c2;
+      }
+      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
+    }
+  };
+
+  const int wm = wid & 1, wn = wid >> 1;
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int LPS = A_PW + B_PW;
+  const int nst = s_end - s_begin;
+  if (nst > 0) issue(s_begin, 0);
+  wait_vm<0>();
+  lds_barrier();
+  for (int i = 0; i < nst; ++i) {
+    const int cur = i & 1;
+    if (i + 1 < nst) issue(s_begin + i + 1, cur ^ 1);
+    const char* As = smem + cur * STAGE;
+    const char* Bs = As + A_BYTES;
+    v8i af[TM], bfr[TN];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) af[m] = frag_tr8<A_ROWB>(As, lane, wm * TM + m);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = frag_tr8<B_ROWB>(Bs, lane, wn * TN + j);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)  // A = dy (e5m2: cbsz 1), B = x (e4m3: blgp 0), unit block scales
+        acc[m][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[j], acc[m][j], 1, 0, 0, 0, 0, 0);
+    if (i + 1 < nst) wait_vm<0>();
+    lds_barrier();
+  }
+  (void)LPS;
+
+  // epilogue: lane (fq, fr) holds kout rows fq*4+e, column fr of each fragment; dequantize, then one
+  // 256-B row segment per atomic wave-instruction through a wave-private LDS image (the drained
+  // pipeline buffers), as the bf16 TN epilogue
+  const float sc = P.dy_deq[0] * P.x_deq[0];
+  const int fq = lane >> 4, fr = lane & 15;
+  float* stg = reinterpret_cast<float*>(smem) + wid * (TM * 16) * 64;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = i * 16 + fq * 4 + e;
+        stg[r * 64 + ((j * 16 + fr) ^ (((r >> 2) & 1) << 4))] = acc[i][j][e] * sc;
+      }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the region is wave-private
+  __builtin_amdgcn_wave_barrier();
+  const int col = c0 + wn * 64 + lane;
+  const int row0 = k0 + wm * TM * 16;
+  if (col < P.Ncols) {
+#pragma unroll 8
+    for (int r = 0; r < TM * 16; ++r) {
+      const float v = stg[r * 64 + (lane ^ (((r >> 2) & 1) << 4))];
+      if (row0 + r < P.Kout) unsafeAtomicAdd(P.out + (int64_t)(row0 + r) * P.Ncols + col, v);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits,
                                                             int64_t n, float* __restrict__ out,
                                                             int accumulate) {
@@ -1865,6 +2070,63 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, dim3(tiles * splits), dim3(CFG::NT), CFG::SMEM, st, a);
   check_launch("igemm_tn");
+}
+
+// fp8 weight gradient (igemm_tn_f8_kernel): split-K planned like plan_wgrad with 128-pixel steps
+void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]) {
+  const int bmg = s.K % 128 == 0 ? 128 : 64;
+  const int ncols = s.R * s.S * s.C;
+  const int tiles = ((s.K + bmg - 1) / bmg) * ((ncols + 127) / 128);
+  const int64_t mred = (int64_t)s.N * s.Ho * s.Wo;
+  const int nsteps = (int)((mred + 127) / 128);
+  int splits = ((tiles <= 4 ? 2048 : 1024) + tiles - 1) / tiles;
+  splits = std::min(splits, std::max(1, nsteps / 8));
+  const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
+  splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, ((int64_t)32 << 20) / dw_bytes));
+  splits = std::max(1, std::min(splits, 1024));
+  const int sps = (nsteps + splits - 1) / splits;
+  out[0] = bmg; out[1] = tiles; out[2] = (nsteps + sps - 1) / sps; out[3] = sps;
+}
+
+void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st) {
+  if (s.C % 16 != 0 || s.K % 64 != 0) throw std::runtime_error("conv_wgrad_fp8: needs C % 16 == 0, K % 64 == 0");
+  int pl[4];
+  conv_wgrad_fp8_plan(s, pl);
+  TnF8Args a{};
+  a.dy = dy8; a.x = x8; a.dy_deq = dy_deq; a.x_deq = x_deq; a.out = dw;
+  a.dy_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K);
+  a.x_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C);
+  a.Mred = s.N * s.Ho * s.Wo; a.Kout = s.K; a.Ncols = s.R * s.S * s.C;
+  a.H = s.H; a.W = s.W; a.C = s.C; a.S = s.S; a.stride = s.stride; a.pad = s.pad; a.stride_w = s.sw();
+  a.HoWo = s.Ho * s.Wo; a.Wo = s.Wo; a.Ho = s.Ho;
+  a.div_hw = make_fastdiv((uint32_t)a.HoWo);
+  a.div_w = make_fastdiv((uint32_t)s.Wo);
+  a.nsteps = (a.Mred + 127) / 128;
+  a.steps_per_split = pl[3];
+  a.adv_r = 128 % s.Wo;
+  a.adv_qh = (128 / s.Wo) % s.Ho;
+  a.adv_qn = (128 / s.Wo) / s.Ho;
+  if (!accumulate) hipMemsetAsync(dw, 0, (size_t)s.K * a.Ncols * sizeof(float), st);
+  const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 && s.H == s.Ho && s.W == s.Wo;
+  const int grid = pl[1] * pl[2];
+  const int smem = 2 * (128 * pl[0] + 128 * 128);
+  static bool attr_set[4] = {false, false, false, false};
+  const int which = (pl[0] == 128 ? 0 : 2) + (pw ? 0 : 1);
+  const void* fn = pl[0] == 128 ? (pw ? (const void*)igemm_tn_f8_kernel<128, true> : (const void*)igemm_tn_f8_kernel<128, false>)
+                                : (pw ? (const void*)igemm_tn_f8_kernel<64, true> : (const void*)igemm_tn_f8_kernel<64, false>);
+  if (!attr_set[which]) {
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set[which] = true;
+  }
+  if (pl[0] == 128) {
+    if (pw) hipLaunchKernelGGL((igemm_tn_f8_kernel<128, true>), dim3(grid), dim3(256), smem, st, a);
+    else hipLaunchKernelGGL((igemm_tn_f8_kernel<128, false>), dim3(grid), dim3(256), smem, st, a);
+  } else {
+    if (pw) hipLaunchKernelGGL((igemm_tn_f8_kernel<64, true>), dim3(grid), dim3(256), smem, st, a);
+    else hipLaunchKernelGGL((igemm_tn_f8_kernel<64, false>), dim3(grid), dim3(256), smem, st, a);
+  }
+  check_launch("igemm_tn_f8");
 }
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,

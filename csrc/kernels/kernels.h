@@ -101,6 +101,11 @@ size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
 void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]);
 // accumulate: dw += wgrad (autograd accumulation semantics; lets the block write straight into
 // the flat gradient buffer), else dw = wgrad.
+// fp8 weight gradient: dw[K][R][S][C] (+)= wgrad(dy8 e5m2 [N,Ho,Wo,K] * dy_deq, x8 e4m3 [N,H,W,C] * x_deq),
+// fp32 atomics (non-deterministic order); C % 16 == 0, K % 64 == 0.  plan: (bmg, tiles, splits, steps/split)
+void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]);
+void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
                        const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st);
 

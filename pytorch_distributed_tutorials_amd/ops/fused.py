@@ -36,6 +36,9 @@ _ZMASK = os.environ.get("PDT_ZMASK", "1") != "0"  # 1-bit ReLU masks for the han
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
 _FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
 _FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input-gradient GEMMs
+# with fp8 backward: weight gradients on the MX-rate MFMA from the e5m2 dy and the e4m3 conv input
+# the forward already produced (igemm_tn_f8_kernel); deterministic runs keep the bf16 slab path
+_FP8_WGRAD = os.environ.get("PDT_FP8_WGRAD", "1") != "0"
 _FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
 _COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
 
@@ -806,6 +809,7 @@ class _ResidualBlock(torch.autograd.Function):
             res = x
         h, h8 = x, x8
         outs = []
+        ins8 = [x8]  # e4m3 copy (q, dequant factor) of each chain unit's conv input, or None
         zmask = None
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
@@ -819,6 +823,8 @@ class _ResidualBlock(torch.autograd.Function):
                                           want_mask=last and tr and _ZMASK and _BN_HANDOFF and _FUSE_DGRAD_BN)
             if last:
                 zmask = zm
+            else:
+                ins8.append(h8)
             outs.append((z, y, stt))
             h = z
         if holder is not None and h8 is not None:
@@ -834,6 +840,7 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.ntensors = len(tensors)
         ctx.handoff_in = handoff  # the producer of x (previous block), or None
         ctx.fp8b = fp8io is not None and _FP8_BWD  # fp8 dgrads in backward (dy in e5m2)
+        ctx.in8 = ins8 if ctx.fp8b and _FP8_WGRAD else None  # fp8 weight-gradient operands
         _, y_last, st_last = outs[-1]
         ctx.handoff_out = _BnHandoff(y_last, st_last, tensors[5 * (nch - 1) + 1],
                                      tensors[5 * (nch - 1) + 2], zmask)
@@ -865,9 +872,24 @@ class _ResidualBlock(torch.autograd.Function):
 
         side = streams.begin(x.device)
 
-        def wgrad(j, dy_, xin_, st_, pd_):
+        in8 = ctx.in8
+        ctx.in8 = None
+
+        def wgrad(j, dy_, xin_, st_, pd_, d8_=None, x8_=None):
             w_ = tensors[j]
             sink = _grad_sink(params[j])
+            k_, c_ = w_.shape[0], w_.shape[1]
+            if (d8_ is not None and x8_ is not None and not det and c_ % 16 == 0 and k_ % 64 == 0
+                    and x8_[0].shape[3] == c_):
+                # e5m2 dy x e4m3 x on the MX-rate MFMA, both already produced for the fp8 GEMMs
+                if sink is not None:
+                    C.conv_wgrad_fp8(side.cuda_stream if side is not None else 0, d8_[0], x8_[0], d8_[1],
+                                     x8_[1], list(w_.shape), st_, pd_, sink)
+                    sunk.append(params[j])
+                else:
+                    grads[j] = C.conv_wgrad_fp8(0, d8_[0], x8_[0], d8_[1], x8_[1], list(w_.shape), st_,
+                                                pd_).to(w_.dtype)
+                return
             if sink is not None:
                 # weight gradient into the flat buffer on the side stream, concurrent with the
                 # dgrad chain; all-reduce and optimizer wait for that stream (streams.py)
@@ -890,11 +912,15 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j + 2] = sums_[0]
             return sums_
 
-        def apply(j, dz_, z_, y_, stt_, sums_, mask_, tr_, want_dres, need_dgrad):
+        def apply(j, dz_, z_, y_, stt_, sums_, mask_, tr_, want_dres, need_dgrad, x8_=None):
             """BN backward apply of unit j -> (dy, dres, d8); d8 = (e5m2 dy, its dequant factor)
-            when the dgrad consuming dy runs on fp8"""
+            when the dgrad consuming dy runs on fp8 (K % 128 == 0), or the weight gradient does
+            (K % 64 == 0 and the conv input's e4m3 copy x8_ exists)"""
             gamma_ = tensors[j + 1]
-            if ctx.fp8b and tr_ and need_dgrad and dz_.shape[3] % 128 == 0:
+            k_ = dz_.shape[3]
+            wgrad8 = (x8_ is not None and not det and k_ % 64 == 0 and tensors[j].shape[1] % 16 == 0
+                      and x8_[0].shape[3] == tensors[j].shape[1])
+            if ctx.fp8b and tr_ and ((need_dgrad and k_ % 128 == 0) or wgrad8):
                 stq = _q8_state(params[j + 1], dz_.device, "_pdt_q8b")
                 slot = stq.next_slot()
                 dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_, y_, stt_, gamma_, sums_, mask_, want_dres,
@@ -904,13 +930,13 @@ class _ResidualBlock(torch.autograd.Function):
             return dy_, dres_, None
 
         def dgrad(dy_, d8_, w_, xshape, st_, pd_, addend_):
-            if d8_ is not None:
+            if d8_ is not None and dy_.shape[3] % 128 == 0:  # a 64-channel dy8 feeds only its wgrad
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
             return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
 
         def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None):
-            if d8_ is not None:
+            if d8_ is not None and dy_.shape[3] % 128 == 0:
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
                                            stt_, mask_, sg, sb)
@@ -936,8 +962,8 @@ class _ResidualBlock(torch.autograd.Function):
             wds = tensors[5 * nch]
             sums_ds = bnreduce(5 * nch, g_short_, g_short_, y_ds, st_ds, 0)
             dy_ds, _, d8_ds = apply(5 * nch, g_short_, g_short_, y_ds, st_ds, sums_ds, 0, tr2, False,
-                                    ctx.needs_input_grad[0])
-            wgrad(5 * nch, dy_ds, x, st2, pd2)
+                                    ctx.needs_input_grad[0], in8[0] if in8 else None)
+            wgrad(5 * nch, dy_ds, x, st2, pd2, d8_ds, in8[0] if in8 else None)
             if not ctx.needs_input_grad[0]:
                 return None
             if st2 == 2 and pd2 == 0 and wds.shape[2] == 1 and wds.shape[3] == 1 and _COMPACT_ADDEND:
@@ -979,13 +1005,13 @@ class _ResidualBlock(torch.autograd.Function):
             if pre is None:
                 mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
                 sums = bnreduce(5 * i, dz, z, y, stt, mask)
-                dy, dres, d8 = apply(5 * i, dz, z, y, stt, sums, mask, tr, last, need_dx)
+                dy, dres, d8 = apply(5 * i, dz, z, y, stt, sums, mask, tr, last, need_dx, in8[i] if in8 else None)
             else:
                 g, sums = pre  # g = dz * relu'(unit i), reduced in the producing epilogue
-                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx)
+                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None)
                 dres = g
             pre = None
-            wgrad(5 * i, dy, xin, st, pd)
+            wgrad(5 * i, dy, xin, st, pd, d8, in8[i] if in8 else None)
             if last:
                 g_short = dres
                 if ds_cfg is not None and nch > 1 and ds_br is not None:

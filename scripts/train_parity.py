@@ -55,8 +55,12 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--window", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fp8", action="store_true",
+                    help="native side on the fp8 path (e4m3 activations / e5m2 gradients, fp8 wgrad)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.fp8:
+        ops.set_fp8(True)
     ds = learnable_dataset(a.samples, 32, 10, device=dev, seed=3, noise=a.noise)
     torch.manual_seed(0)
     stock = build_model("resnet18", num_classes=10).to(dev)

@@ -14,12 +14,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def test_native_bf16_training_tracks_stock_fp32(gpu, tmp_path):
+@pytest.mark.parametrize("fp8", [False, True])
+def test_native_training_tracks_stock_fp32(gpu, tmp_path, fp8):
+    """bf16, and the fp8 path (e4m3 forward GEMMs, e5m2 input gradients, fp8 weight gradients)."""
     out = tmp_path / "parity.json"
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_parity.py"), "--steps", "200",
-                        "--json", str(out)], cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+                        "--json", str(out)] + (["--fp8"] if fp8 else []), cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=200)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert res["finite"]

@@ -156,6 +156,40 @@ def _deq(q, fmt):
     return q.view(torch.float8_e4m3fn if fmt == 4 else torch.float8_e5m2).float()
 
 
+# fp8 weight gradient (igemm_tn_f8_kernel): every loader / tile variant it has
+WGRAD_F8_PLANS = [
+    ((16, 56, 56, 64, 256, 1, 1, 1, 0), 128),    # pointwise loader, 128-row tile
+    ((16, 28, 28, 128, 128, 3, 3, 1, 1), 128),   # 3x3 general loader (halo taps, padding)
+    ((16, 56, 56, 64, 64, 3, 3, 1, 1), 64),      # Kout = 64: 64-row tile
+    ((16, 28, 28, 256, 512, 1, 1, 2, 0), 128),   # strided 1x1 (general loader)
+    ((8, 7, 7, 512, 512, 3, 3, 1, 1), 128),      # 7x7: reduction not a multiple of the 128-pixel step
+]
+
+
+@pytest.mark.parametrize("shape,bm", WGRAD_F8_PLANS)
+def test_fp8_wgrad_per_plan(gpu, native_ext, shape, bm):
+    """e5m2 dy x e4m3 x on the MX-rate MFMA vs fp32 conv2d_nhwc_wgrad of the dequantised operands,
+    into a fresh tensor and accumulated into a KRSC sink (the flat-gradient path)."""
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, dy = _operands(shape, gpu, 6)
+    plan = C.conv_wgrad_fp8_plan(list(x.shape), list(wt.shape), st, pd)
+    assert plan["bm"] == bm
+    x = torch.relu(x.float())
+    xs, ds = 2.0 ** 3, 2.0 ** 12
+    x8 = (x * xs).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
+    d8 = (dy.float() * 1e-3 * ds).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8).contiguous()
+    xq, dq = torch.tensor([1.0 / xs], device=gpu), torch.tensor([1.0 / ds], device=gpu)
+    ref_dw = ref.conv2d_nhwc_wgrad((_deq(d8, 5) / ds).to(torch.bfloat16), (_deq(x8, 4) / xs).to(torch.bfloat16),
+                                   wt.shape, st, pd)
+    dw = C.conv_wgrad_fp8(0, d8, x8, dq, xq, list(wt.shape), st, pd)
+    assert _rel(dw, ref_dw) < 2e-2
+    sink = torch.randn(k, r, s, c, device=gpu).permute(0, 3, 1, 2)  # KRSC-dense [K,C,R,S] view
+    base = sink.clone()
+    C.conv_wgrad_fp8(0, d8, x8, dq, xq, list(wt.shape), st, pd, sink)
+    assert _rel(sink - base, ref_dw) < 2e-2
+
+
 def test_fp8_fwd_and_dgrad_on_wide_tile(gpu, native_ext):
     from pytorch_distributed_tutorials_amd.ops.fused import _packed_crsk8
     C = native_ext
