@@ -751,7 +751,7 @@ std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, c
 std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const Tensor& z, const Tensor& y,
                                                        const Tensor& stats, const Tensor& gamma,
                                                        const Tensor& sums, int64_t mask, bool want_dres,
-                                                       Tensor state, int64_t slot) {
+                                                       Tensor state, int64_t slot, bool want_dy) {
   check_bf16_nhwc(dz, "dz");
   check_bf16_nhwc(y, "y");
   check_state(state, slot);
@@ -761,13 +761,13 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const T
   TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
   if (mask == 1) check_bf16_nhwc(z, "z");
   int64_t M = y.numel() / K;
-  auto dy = at::empty_like(dz);
-  Tensor dres;
+  Tensor dy, dres;
+  if (want_dy) dy = at::empty_like(dz);  // else: fp8-only dy, every consumer reads dy8
   if (want_dres) dres = at::empty_like(dz);
   auto dy8 = at::empty(dz.sizes(), dz.options().dtype(at::kByte));
   pdt::launch_bn_act_bwd_apply_q8(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
                                   gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)mask, true, M, K,
-                                  bf(dy), want_dres ? bf(dres) : nullptr, dy8.data_ptr<uint8_t>(),
+                                  want_dy ? bf(dy) : nullptr, want_dres ? bf(dres) : nullptr, dy8.data_ptr<uint8_t>(),
                                   state.data_ptr<float>(), (int)slot, cur_stream(dz));
   return {dy, dres, dy8};
 }
@@ -1152,7 +1152,7 @@ Tensor quant_e4m3(const Tensor& x, Tensor state, int64_t slot) {
 // (z, q, zmask); zmask is undefined unless want_mask (needs relu)
 std::tuple<Tensor, Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& scale, const Tensor& shift,
                                                  const std::optional<Tensor>& res, bool relu, Tensor state,
-                                                 int64_t slot, bool want_mask) {
+                                                 int64_t slot, bool want_mask, bool want_z) {
   check_bf16_nhwc(y, "y");
   check_state(state, slot);
   c10::hip::HIPGuard g(y.get_device());
@@ -1165,11 +1165,13 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& 
     rp = cbf(*res);
   }
   TORCH_CHECK(!want_mask || relu, "a ReLU mask needs relu");
-  auto z = at::empty_like(y);
+  Tensor z;
+  if (want_z) z = at::empty_like(y);  // else: fp8-only activation, every consumer reads q
   auto q = at::empty(y.sizes(), y.options().dtype(at::kByte));
   Tensor zm;
   if (want_mask) zm = at::empty({y.numel() / 8}, y.options().dtype(at::kByte));
-  pdt::launch_bn_act_fwd_q8(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z),
+  pdt::launch_bn_act_fwd_q8(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu,
+                            want_z ? bf(z) : nullptr,
                             q.data_ptr<uint8_t>(), M, K, state.data_ptr<float>(), (int)slot, cur_stream(y),
                             want_mask ? zm.data_ptr<uint8_t>() : nullptr);
   return {z, q, zm};
@@ -1309,7 +1311,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fp8_deq_offset", &pdt::fp8_deq_offset);
   m.def("bn_act_fwd_q8", checked("bn_act_fwd_q8", &bn_act_fwd_q8), py::arg("y"), py::arg("scale"),
         py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"),
-        py::arg("want_mask") = false);
+        py::arg("want_mask") = false, py::arg("want_z") = true);
   m.def("conv_fwd_fp8", checked("conv_fwd_fp8", &conv_fwd_fp8), py::arg("x"), py::arg("wq"), py::arg("oscale"),
         py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("ascale") = py::none());
   m.def("conv_dgrad_fp8", checked("conv_dgrad_fp8", &conv_dgrad_fp8), py::arg("dy8"), py::arg("wt8"),
@@ -1319,7 +1321,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wscale"), py::arg("ascale"), py::arg("x_shape"), py::arg("stride"), py::arg("pad"),
         py::arg("addend"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
-  m.def("bn_act_bwd_apply_q8", checked("bn_act_bwd_apply_q8", &bn_act_bwd_apply_q8));
+  m.def("bn_act_bwd_apply_q8", checked("bn_act_bwd_apply_q8", &bn_act_bwd_apply_q8), py::arg("dz"), py::arg("z"),
+        py::arg("y"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("mask"), py::arg("want_dres"),
+        py::arg("state"), py::arg("slot"), py::arg("want_dy") = true);
   m.def("quant_rows_e4m3", checked("quant_rows_e4m3", &quant_rows_e4m3));
   m.def("quant_rows_entry_bytes", []() { return (int64_t)pdt::quant_rows_entry_bytes(); });
   m.def("mfma_f8_probe", checked("mfma_f8_probe", &mfma_f8_probe), py::arg("a"), py::arg("b"),

@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       o.v[j] = TRAIN ? k1[j] * (g - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * g;
     }
     const uint4 ob = pack8(o);
-    dy[v] = ob;
+    if (!Q8 || dy != nullptr) dy[v] = ob;  // Q8 with dy null: fp8-only dy (every consumer reads dy8)
     if (DRES) dres[v] = pack8(gr);
     if constexpr (Q8) {
       const f8 r = unpack8(ob);  // quantize exactly the bf16 dy the weight gradient reads

@@ -39,6 +39,9 @@ _FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input
 # with fp8 backward: weight gradients on the MX-rate MFMA from the e5m2 dy and the e4m3 conv input
 # the forward already produced (igemm_tn_f8_kernel); deterministic runs keep the bf16 slab path
 _FP8_WGRAD = os.environ.get("PDT_FP8_WGRAD", "1") != "0"
+# fp8-only storage: activations / input gradients whose every consumer reads the fp8 copy are not
+# written in bf16 at all (interior bottleneck outputs, and dy of convs with fp8 dgrad + fp8 wgrad)
+_FP8_ONLY = os.environ.get("PDT_FP8_ONLY", "1") != "0"
 _FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
 _COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
 
@@ -697,7 +700,7 @@ def _packed_crsk(w):
 
 
 def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual,
-              x8=None, q8=None, want_mask=False):
+              x8=None, q8=None, want_mask=False, want_z=True):
     """conv -> BN -> (+residual) -> (ReLU) -> (z, y, stats, z8, zmask).  x8 = (e4m3 copy of x, its
     dequant factor): fp8 conv; q8 = _Q8State: also emit the e4m3 copy z8 of the output;
     want_mask (with relu): also the 1-bit ReLU mask zmask a later BN-fused dgrad reads instead of z.
@@ -713,7 +716,7 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     if q8 is not None and k % 16 == 0:
         assert rsc is None, "fp8 apply takes a materialised residual"
         slot = q8.next_slot()
-        z, zq, zm = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot, want_mask)
+        z, zq, zm = C.bn_act_fwd_q8(y, stats[2], stats[3], residual, relu, q8.buf, slot, want_mask, want_z)
         return z, y, stats, (zq, q8.deq(slot)), (zm if want_mask else None)
     if want_mask:
         z, zm = C.bn_act_fwd_mask(y, stats[2], stats[3], residual, rsc, rsh)
@@ -722,12 +725,27 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     return z, y, stats, None, None
 
 
+def _fp8_conv_ok(r, s, cx):
+    """fp8 forward conv for a GEMM K of r*s*cx (below 256 the 128-wide fp8 K-step is half empty)."""
+    return r * s * cx >= 256
+
+
+def _fp8_only_ok(w_next, k, tr):
+    """May unit output z (k channels, training) skip its bf16 copy?  Only when every reader takes the
+    e4m3 copy: the next conv's forward GEMM and its fp8 weight gradient (backward masks of interior
+    units are recomputed from y, so z itself is never read there)."""
+    if not (tr and _FP8_BWD and _FP8_WGRAD and _FP8_ONLY) or deterministic():
+        return False
+    kn, cn, rn, sn = w_next.shape
+    return cn == k and k % 16 == 0 and kn % 64 == 0 and _fp8_conv_ok(rn, sn, k)
+
+
 def _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, momentum, eps, x8=None):
     """conv -> BN statistics (finalize, running-stat update): (y, stats[4, K])."""
     k, _, r, s = w.shape
-    n, h, wd, cx = x.shape
+    n, h, wd, cx = (x if x is not None else x8[0]).shape  # x None: an fp8-only activation
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
-    if x8 is not None and r * s * cx < 256:
+    if x8 is not None and not _fp8_conv_ok(r, s, cx) and x is not None:
         x8 = None  # a GEMM K of 64 (1x1 over 64 channels) half-fills the 128-wide fp8 K-step: bf16 is faster
     if x8 is not None:
         wq, wsc = _packed_krsc8(C, w, cx)
@@ -818,9 +836,13 @@ class _ResidualBlock(torch.autograd.Function):
                 ds_join[0].wait_event(ds_join[1])
             # the block output's ReLU mask as bits: the next block's BN-fused dgrad reads it
             # instead of z (1/16 of the bytes)
+            want_z = last or q8s is None or not _fp8_only_ok(tensors[5 * (i + 1)], w.shape[0], tr)
             z, y, stt, h8, zm = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
                                           res if last else None, h8, q8s[i] if q8s else None,
-                                          want_mask=last and tr and _ZMASK and _BN_HANDOFF and _FUSE_DGRAD_BN)
+                                          want_mask=last and tr and _ZMASK and _BN_HANDOFF and _FUSE_DGRAD_BN,
+                                          want_z=want_z)
+            if z is None and h8 is None:
+                raise RuntimeError("fp8-only activation without its e4m3 copy")
             if last:
                 zmask = zm
             else:
@@ -890,6 +912,8 @@ class _ResidualBlock(torch.autograd.Function):
                     grads[j] = C.conv_wgrad_fp8(0, d8_[0], x8_[0], d8_[1], x8_[1], list(w_.shape), st_,
                                                 pd_).to(w_.dtype)
                 return
+            if dy_ is None or xin_ is None:
+                raise RuntimeError("fp8-only operands reached the bf16 weight gradient")
             if sink is not None:
                 # weight gradient into the flat buffer on the side stream, concurrent with the
                 # dgrad chain; all-reduce and optimizer wait for that stream (streams.py)
@@ -902,6 +926,9 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j] = C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det).to(w_.dtype)
 
         def bnreduce(j, dz_, z_, y_, stt_, mask_):
+            if z_ is None:  # fp8-only z: interior units recompute the ReLU mask from y (mask 2)
+                assert mask_ != 1
+                z_ = y_
             sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
             if sg is not None and sb is not None:
                 sums_ = C.bn_act_bwd_reduce(dz_, z_, y_, stt_, mask_, sg, sb)
@@ -923,20 +950,23 @@ class _ResidualBlock(torch.autograd.Function):
             if ctx.fp8b and tr_ and ((need_dgrad and k_ % 128 == 0) or wgrad8):
                 stq = _q8_state(params[j + 1], dz_.device, "_pdt_q8b")
                 slot = stq.next_slot()
-                dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_, y_, stt_, gamma_, sums_, mask_, want_dres,
-                                                       stq.buf, slot)
+                # fp8-only dy: the dgrad (if any) and the weight gradient both read the e5m2 copy
+                want_dy = not (_FP8_ONLY and wgrad8 and (not need_dgrad or k_ % 128 == 0))
+                dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_ if z_ is not None else y_, y_, stt_, gamma_,
+                                                       sums_, mask_, want_dres, stq.buf, slot, want_dy)
                 return dy_, dres_, (q_, stq.deq(slot))
-            dy_, dres_ = C.bn_act_bwd_apply(dz_, z_, y_, stt_, gamma_, sums_, mask_, tr_, want_dres)
+            dy_, dres_ = C.bn_act_bwd_apply(dz_, z_ if z_ is not None else y_, y_, stt_, gamma_, sums_, mask_,
+                                            tr_, want_dres)
             return dy_, dres_, None
 
         def dgrad(dy_, d8_, w_, xshape, st_, pd_, addend_):
-            if d8_ is not None and dy_.shape[3] % 128 == 0:  # a 64-channel dy8 feeds only its wgrad
+            if d8_ is not None and d8_[0].shape[3] % 128 == 0:  # a 64-channel dy8 feeds only its wgrad
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
             return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
 
         def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None):
-            if d8_ is not None and dy_.shape[3] % 128 == 0:
+            if d8_ is not None and d8_[0].shape[3] % 128 == 0:
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
                                            stt_, mask_, sg, sb)
@@ -999,7 +1029,8 @@ class _ResidualBlock(torch.autograd.Function):
             st, pd, tr, mo, ep = chain[i]
             z, y, stt = units[i]
             w, gamma = tensors[5 * i], tensors[5 * i + 1]
-            xin = x if i == 0 else units[i - 1][0]
+            xin = x if i == 0 else units[i - 1][0]  # None: fp8-only (its e4m3 copy is in8[i])
+            xin_shape = list((xin if xin is not None else units[i - 1][1]).shape)
             last = i == nch - 1
             need_dx = i > 0 or ctx.needs_input_grad[0]
             if pre is None:
@@ -1024,9 +1055,9 @@ class _ResidualBlock(torch.autograd.Function):
             if i > 0:
                 yp, sttp = units[i - 1][1], units[i - 1][2]
                 if _FUSE_DGRAD_BN:
-                    pre = dgrad_bn(5 * (i - 1), dy, d8, w, list(xin.shape), st, pd, None, yp, None, sttp, 2)
+                    pre = dgrad_bn(5 * (i - 1), dy, d8, w, xin_shape, st, pd, None, yp, None, sttp, 2)
                 else:
-                    dz = dgrad(dy, d8, w, list(xin.shape), st, pd, None)
+                    dz = dgrad(dy, d8, w, xin_shape, st, pd, None)
             else:
                 # shortcut gradient: identity -> g_short itself; projection -> its dgrad
                 if ds_join is not None:
