@@ -332,7 +332,9 @@ def test_resnet50_fp8_dgrad_matches_bf16_dgrad_on_same_forward(gpu, native_ext):
         ops.set_fp8(True)
         fused._FP8_BWD = bwd8
         try:
-            for _ in range(3):  # delayed scaling: later calls use real amax history
+            # delayed scaling: later calls use real amax history; the scales settle after one call
+            # per quantized layer in a dependency chain (4 calls on this net, scripts/diag_fp8_det.py)
+            for _ in range(6):
                 ddp.space.zero_grad()
                 loss = ops.cross_entropy(ddp(x), yl)
                 loss.backward()
