@@ -26,8 +26,14 @@ namespace pdt {
 // (exact decomposition of the total sum of squares; only plain sums -> fully parallel, no
 // serial divide chain).  Stage 1: block (32 channels, partition p of FIN_GPB groups);
 // stage 2: per channel sum over partitions, fixed order (deterministic).
-constexpr int FIN_CH = 32;
-constexpr int FIN_ROWS = 8;                 // threads per channel in a block
+// Block shape (PDT_FIN_CH channels x 256/PDT_FIN_CH group rows): a tall block gives each thread
+// fewer dependent partial loads (the reduction is latency-bound: ~100 of these tiny launches sit
+// on the critical path of a ResNet-50 step).
+#ifndef PDT_FIN_CH
+#define PDT_FIN_CH 32
+#endif
+constexpr int FIN_CH = PDT_FIN_CH;
+constexpr int FIN_ROWS = 256 / FIN_CH;      // threads per channel in a block
 constexpr int FIN_GPB = FIN_ROWS * 16;      // groups per block (16 independent loads per thread)
 // Up to FIN_SINGLE groups, ONE block per 32-channel tile reads them all and finishes in place:
 // no partial round trip and no last-block handshake (a dependent sc1 store / atomic / sc1 load

@@ -24,9 +24,14 @@ namespace pdt {
 typedef __bf16 fc_v8bf __attribute__((ext_vector_type(8)));
 
 // LDS image of one operand tile: [64 rows][32 k] bf16, 80-byte row pitch (64 B + 16 B pad: the
-// 16 lanes of a fragment read hit 16 different 16-byte bank slots)
+// 16 lanes of a fragment read hit 16 different 16-byte bank slots), and the 16-B k-chunk of row r
+// stored at chunk ^ ((r >> 4) & 3): constant over a fragment's 16 rows (reads unchanged), but the
+// transposing store of a k-strided operand -- 8 row groups x 4 dwords per wave instruction, whose
+// unswizzled rows 8 apart all fell on 2 bank offsets (4-way conflicts, 10-12 conflict cycles per
+// LDS instruction measured, profiles/r2s2_sq_mfma_busy_per_kernel.txt) -- now hits 32 distinct banks
 constexpr int FC_PITCH = 80;
 constexpr int FC_TILE_BYTES = 64 * FC_PITCH;
+__device__ __forceinline__ int fc_off(int row, int chunk) { return row * FC_PITCH + ((chunk ^ ((row >> 4) & 3)) << 4); }
 
 // Global -> register stage of one operand tile (64 rows x 32 k, fp32): 8 values per thread.
 // KC (k-contiguous): thread t holds row t/4, k 8*(t%4)..+7 (two 16-byte loads);
@@ -67,12 +72,12 @@ struct FcStage {
       fc_v8bf f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = (__bf16)v[j];
-      *reinterpret_cast<fc_v8bf*>(lds + (t / 4) * FC_PITCH + (t % 4) * 16) = f;
+      *reinterpret_cast<fc_v8bf*>(lds + fc_off(t / 4, t % 4)) = f;
     } else {
       const int k = t / 8, r = (t % 8) * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        *reinterpret_cast<__bf16*>(lds + (r + j) * FC_PITCH + k * 2) = (__bf16)v[j];
+        *reinterpret_cast<__bf16*>(lds + fc_off(r + j, k >> 3) + (k & 7) * 2) = (__bf16)v[j];
     }
   }
   __device__ __forceinline__ void add_rows(float (&rs)[8]) const {  // row-contiguous stage only
@@ -129,10 +134,10 @@ __global__ void __launch_bounds__(256) fc_gemm_kernel(const FcArgs p) {
     v4i af[2], bfr[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      af[i] = *reinterpret_cast<const v4i*>(As + (wm * 32 + i * 16 + fr) * FC_PITCH + fq * 16);
+      af[i] = *reinterpret_cast<const v4i*>(As + fc_off(wm * 32 + i * 16 + fr, fq));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      bfr[j] = *reinterpret_cast<const v4i*>(Bs + (wn * 32 + j * 16 + fr) * FC_PITCH + fq * 16);
+      bfr[j] = *reinterpret_cast<const v4i*>(Bs + fc_off(wn * 32 + j * 16 + fr, fq));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
