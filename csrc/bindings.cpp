@@ -213,7 +213,8 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
                                          const std::optional<Tensor>& addend, const Tensor& y,
                                          const std::optional<Tensor>& z, const Tensor& stats, int64_t mask,
                                          const std::optional<Tensor>& dgamma,
-                                         const std::optional<Tensor>& dbeta, Launch&& launch) {
+                                         const std::optional<Tensor>& dbeta, const std::optional<Tensor>& acc,
+                                         Launch&& launch) {
   check_bf16_nhwc(y, "y");
   TORCH_CHECK(y.size(0) == s.N && y.size(1) == s.H && y.size(2) == s.W && y.size(3) == s.C,
               "dgrad_bn: y must have the shape of x");
@@ -239,6 +240,18 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
     asub = addend_layout(*addend, dx);
     ap = cbf(*addend);
   }
+  hipStream_t st = cur_stream(dy_like);
+  if (acc.has_value() && acc->defined()) {
+    // partials fp32-atomically summed by the epilogue into the caller's zeroed [2][C] accumulator:
+    // no partial buffer, no reduce launch; the BN parameter gradients are added by the consuming
+    // bn_act_bwd_apply(dgamma=, dbeta=), which runs after the sums are complete
+    TORCH_CHECK(acc->is_cuda() && acc->scalar_type() == at::kFloat && acc->is_contiguous() &&
+                acc->numel() == 2 * s.C, "acc must be a contiguous fp32 [2, C] device tensor");
+    TORCH_CHECK(!(dgamma.has_value() && dgamma->defined()), "acc mode: pass dgamma/dbeta to the apply");
+    pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), nullptr, (int)mask, acc->data_ptr<float>()};
+    launch(s, bf(dx), ap, &bn, st, asub);
+    return {dx, acc->view({2, s.C})};
+  }
   const int G = pdt::conv_dgrad_bn_groups(s, (int)dy_like.element_size());
   auto fopt = y.options().dtype(at::kFloat);
   // sums, partials and the reduction workspace as slices of ONE allocation (host issue: each
@@ -250,7 +263,6 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
   auto part = fbuf.narrow(0, n_sums, n_part);
   auto ws = fbuf.narrow(0, n_sums + n_part, n_ws);
   pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
-  hipStream_t st = cur_stream(dy_like);
   launch(s, bf(dx), ap, &bn, st, asub);
   float* dg = nullptr;
   float* db = nullptr;
@@ -272,7 +284,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
                                          const std::optional<Tensor>& z, const Tensor& stats,
                                          int64_t mask, const std::optional<Tensor>& dgamma,
                                          const std::optional<Tensor>& dbeta,
-                                         const std::optional<Tensor>& wt_in) {
+                                         const std::optional<Tensor>& wt_in, const std::optional<Tensor>& acc) {
   check_bf16_nhwc(dy, "dy");
   TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
   TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
@@ -280,7 +292,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
   auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
   Tensor wt = packed_t_or_pack(w, wt_in);
-  return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta,
+  return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta, acc,
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad(cbf(dy), cbf(wt), dx, ap, sh, st, bn, asub);
@@ -328,10 +340,11 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fp8(const Tensor& dy8, const Tensor& wt
                                              const Tensor& y, const std::optional<Tensor>& z,
                                              const Tensor& stats, int64_t mask,
                                              const std::optional<Tensor>& dgamma,
-                                             const std::optional<Tensor>& dbeta) {
+                                             const std::optional<Tensor>& dbeta,
+                                             const std::optional<Tensor>& acc) {
   c10::hip::HIPGuard g(dy8.get_device());
   auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
-  return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta,
+  return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta, acc,
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(),
@@ -384,7 +397,8 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
 // wait_stream + stream context + two record_stream calls: ~25 us of host issue per weight
 // gradient (scripts/host_profile.py), 20-53 of them per step.
 Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vector<int64_t> ws,
-                       int64_t stride, int64_t pad, bool deterministic, const std::optional<Tensor>& out) {
+                       int64_t stride, int64_t pad, bool deterministic, const std::optional<Tensor>& out,
+                       const std::optional<Tensor>& zero) {
   TORCH_CHECK(side != 0, "conv_wgrad_side: null side stream");
   c10::hip::HIPGuard g(x.get_device());
   const auto dev = (c10::DeviceIndex)x.get_device();
@@ -401,6 +415,10 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
   {
     c10::hip::HIPStreamGuard sg(sst);
     r = conv_wgrad(dy, x, ws, stride, pad, deterministic, out);
+    // `zero`: a BN-sum accumulator whose consumer (the apply just queued on the current stream) is
+    // done at this point of the side stream: re-zeroed here, off the critical path, for its next use
+    if (zero.has_value() && zero->defined())
+      TORCH_CHECK(hipMemsetAsync(zero->data_ptr(), 0, zero->nbytes(), sst.stream()) == hipSuccess, "memset");
   }
   c10::hip::HIPCachingAllocator::recordStream(dy.storage().data_ptr(), sst);
   c10::hip::HIPCachingAllocator::recordStream(x.storage().data_ptr(), sst);
@@ -412,7 +430,8 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
 // view, e.g. the flat gradient buffer) or returns a fresh [K,C,R,S] channels_last tensor.  side != 0:
 // issued on that stream after the current stream's queued work, like conv_wgrad_side.
 Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const Tensor& dy_deq, const Tensor& x_deq,
-                      std::vector<int64_t> ws, int64_t stride, int64_t pad, const std::optional<Tensor>& out) {
+                      std::vector<int64_t> ws, int64_t stride, int64_t pad, const std::optional<Tensor>& out,
+                      const std::optional<Tensor>& zero) {
   TORCH_CHECK(dy8.is_cuda() && x8.is_cuda() && dy8.scalar_type() == at::kByte && x8.scalar_type() == at::kByte &&
               dy8.dim() == 4 && x8.dim() == 4 && dy8.is_contiguous() && x8.is_contiguous(),
               "conv_wgrad_fp8: dy8 / x8 must be contiguous uint8 NHWC device tensors");
@@ -457,6 +476,8 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
                                x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st);
     r = dwp.permute({0, 3, 1, 2});
   }
+  if (zero.has_value() && zero->defined())  // as conv_wgrad_side: a consumed BN-sum accumulator
+    TORCH_CHECK(hipMemsetAsync(zero->data_ptr(), 0, zero->nbytes(), st) == hipSuccess, "memset");
   if (side != 0) {
     auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
     for (const Tensor* t : {&dy8, &x8, &dy_deq, &x_deq})
@@ -726,10 +747,25 @@ Tensor bn_act_bwd_reduce(const Tensor& dz, const Tensor& z, const Tensor& y, con
   return sums;
 }
 
+// optional BN parameter-gradient sinks (fp32 [K], both or neither)
+static std::pair<float*, float*> bn_param_sinks(const std::optional<Tensor>& dgamma,
+                                                const std::optional<Tensor>& dbeta, int64_t K) {
+  if (!(dgamma.has_value() && dgamma->defined())) {
+    TORCH_CHECK(!(dbeta.has_value() && dbeta->defined()), "dgamma and dbeta go together");
+    return {nullptr, nullptr};
+  }
+  TORCH_CHECK(dbeta.has_value() && dbeta->defined(), "dgamma and dbeta go together");
+  TORCH_CHECK(dgamma->is_contiguous() && dbeta->is_contiguous() && dgamma->numel() == K &&
+              dbeta->numel() == K && dgamma->scalar_type() == at::kFloat && dbeta->scalar_type() == at::kFloat,
+              "dgamma/dbeta: fp32 [C]");
+  return {dgamma->data_ptr<float>(), dbeta->data_ptr<float>()};
+}
+
 std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, const Tensor& y,
                                             const Tensor& stats, const Tensor& gamma,
                                             const Tensor& sums, int64_t mask, bool training,
-                                            bool want_dres) {
+                                            bool want_dres, const std::optional<Tensor>& dgamma,
+                                            const std::optional<Tensor>& dbeta) {
   check_bf16_nhwc(dz, "dz");
   check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(dz.get_device());
@@ -741,9 +777,11 @@ std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, c
   auto dy = at::empty_like(dz);
   Tensor dres;
   if (want_dres) dres = at::empty_like(dz);
+  auto pg = bn_param_sinks(dgamma, dbeta, K);
   pdt::launch_bn_act_bwd_apply(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
                                gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)mask, training,
-                               M, K, bf(dy), want_dres ? bf(dres) : nullptr, cur_stream(dz));
+                               M, K, bf(dy), want_dres ? bf(dres) : nullptr, cur_stream(dz), pg.first,
+                               pg.second);
   return {dy, dres};
 }
 
@@ -751,7 +789,9 @@ std::tuple<Tensor, Tensor> bn_act_bwd_apply(const Tensor& dz, const Tensor& z, c
 std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const Tensor& z, const Tensor& y,
                                                        const Tensor& stats, const Tensor& gamma,
                                                        const Tensor& sums, int64_t mask, bool want_dres,
-                                                       Tensor state, int64_t slot, bool want_dy) {
+                                                       Tensor state, int64_t slot, bool want_dy,
+                                                       const std::optional<Tensor>& dgamma,
+                                                       const std::optional<Tensor>& dbeta) {
   check_bf16_nhwc(dz, "dz");
   check_bf16_nhwc(y, "y");
   check_state(state, slot);
@@ -761,6 +801,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const T
   TORCH_CHECK(stats.numel() == 4 * K && stats.is_contiguous(), "stats must be [4, K]");
   if (mask == 1) check_bf16_nhwc(z, "z");
   int64_t M = y.numel() / K;
+  auto pg = bn_param_sinks(dgamma, dbeta, K);
   Tensor dy, dres;
   if (want_dy) dy = at::empty_like(dz);  // else: fp8-only dy, every consumer reads dy8
   if (want_dres) dres = at::empty_like(dz);
@@ -768,7 +809,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_bwd_apply_q8(const Tensor& dz, const T
   pdt::launch_bn_act_bwd_apply_q8(cbf(dz), mask == 1 ? cbf(z) : nullptr, cbf(y), stats.data_ptr<float>(),
                                   gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)mask, true, M, K,
                                   want_dy ? bf(dy) : nullptr, want_dres ? bf(dres) : nullptr, dy8.data_ptr<uint8_t>(),
-                                  state.data_ptr<float>(), (int)slot, cur_stream(dz));
+                                  state.data_ptr<float>(), (int)slot, cur_stream(dz), pg.first, pg.second);
   return {dy, dres, dy8};
 }
 
@@ -1239,15 +1280,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad_bn", checked("conv_dgrad_bn", &conv_dgrad_bn), py::arg("dy"), py::arg("w"),
         py::arg("x_shape"), py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("y"),
         py::arg("z"), py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(),
-        py::arg("dbeta") = py::none(), py::arg("wt") = py::none());
+        py::arg("dbeta") = py::none(), py::arg("wt") = py::none(), py::arg("acc") = py::none());
   m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
   m.def("conv_wgrad_side", checked("conv_wgrad_side", &conv_wgrad_side), py::arg("side"), py::arg("dy"),
         py::arg("x"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"), py::arg("deterministic") = false,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("zero") = py::none());
   m.def("conv_wgrad_fp8", checked("conv_wgrad_fp8", &conv_wgrad_fp8), py::arg("side"), py::arg("dy8"),
         py::arg("x8"), py::arg("dy_deq"), py::arg("x_deq"), py::arg("w_shape"), py::arg("stride"), py::arg("pad"),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("zero") = py::none());
   m.def("conv_wgrad_fp8_plan", [](std::vector<int64_t> x_shape, std::vector<int64_t> w_shape, int stride, int pad) {
     pdt::ConvShape s = shape_of((int)x_shape[0], (int)x_shape[1], (int)x_shape[2], (int)x_shape[3], (int)w_shape[0],
                                 (int)w_shape[2], (int)w_shape[3], stride, pad);
@@ -1278,7 +1319,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("res_shift") = py::none());
   m.def("bn_act_bwd_reduce", checked("bn_act_bwd_reduce", &bn_act_bwd_reduce), py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
-  m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply));
+  m.def("bn_act_bwd_apply", checked("bn_act_bwd_apply", &bn_act_bwd_apply), py::arg("dz"), py::arg("z"),
+        py::arg("y"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("mask"), py::arg("training"),
+        py::arg("want_dres"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("augment", checked("augment", &augment), py::arg("images"), py::arg("idx"), py::arg("oy"), py::arg("ox"),
         py::arg("flip"), py::arg("pad"), py::arg("normalize"), py::arg("mean"), py::arg("std"));
   m.def("maxpool_fwd", checked("maxpool_fwd", &maxpool_fwd));
@@ -1320,10 +1363,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad_bn_fp8", checked("conv_dgrad_bn_fp8", &conv_dgrad_bn_fp8), py::arg("dy8"), py::arg("wt8"),
         py::arg("wscale"), py::arg("ascale"), py::arg("x_shape"), py::arg("stride"), py::arg("pad"),
         py::arg("addend"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
-        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(), py::arg("acc") = py::none());
   m.def("bn_act_bwd_apply_q8", checked("bn_act_bwd_apply_q8", &bn_act_bwd_apply_q8), py::arg("dz"), py::arg("z"),
         py::arg("y"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("mask"), py::arg("want_dres"),
-        py::arg("state"), py::arg("slot"), py::arg("want_dy") = true);
+        py::arg("state"), py::arg("slot"), py::arg("want_dy") = true, py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
   m.def("quant_rows_e4m3", checked("quant_rows_e4m3", &quant_rows_e4m3));
   m.def("quant_rows_entry_bytes", []() { return (int64_t)pdt::quant_rows_entry_bytes(); });
   m.def("mfma_f8_probe", checked("mfma_f8_probe", &mfma_f8_probe), py::arg("a"), py::arg("b"),

@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ sums, int64_t nvec, int K8, float invM, uint4* __restrict__ dy,
     uint4* __restrict__ dres, uint2* __restrict__ dy8 = nullptr, float* __restrict__ state = nullptr,
-    int slot = 0) {
+    int slot = 0, float* __restrict__ dgamma = nullptr, float* __restrict__ dbeta = nullptr) {
   const int K = K8 * 8;
   float qs = 1.f, qm = 0.f;
   if constexpr (Q8) {
@@ -631,6 +631,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       k1[j] = gm[j] * is[j];
       sgm[j] = s0[j] * invM;                 // mean of g
       k2[j] = s1[j] * is[j] * is[j] * invM;  // mean of g*xhat, divided by std
+    }
+    // BN parameter gradients from the finished sums (sums accumulated by the producing dgrad's
+    // epilogue atomics: no separate reduce launch): one thread per 8-channel group
+    if (dgamma != nullptr && tid < K8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dgamma[c0 + j] += s1[j] * is[j];
+        dbeta[c0 + j] += s0[j];
+      }
     }
   }
   for (int64_t v = tid; v < nvec; v += stride) {
@@ -666,7 +675,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
 void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                              const float* stats, const float* gamma, const float* sums, int mask,
                              bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
-                             hipStream_t st) {
+                             hipStream_t st, float* dgamma, float* dbeta) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
   dim3 g(ew_blocks(nvec, K8)), b(256);
@@ -678,7 +687,7 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   float invM = 1.f / (float)M;
 #define PDT_BWD(MK, TR, DRS)                                                                  \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, TR, DRS>), g, b, 0, st, DZ, Z, Y, stats, gamma, \
-                     sums, nvec, K8, invM, DY, DR)
+                     sums, nvec, K8, invM, DY, DR, nullptr, nullptr, 0, dgamma, dbeta)
 #define PDT_BWD_T(MK)                                                             \
   if (training) { if (dres) PDT_BWD(MK, true, true); else PDT_BWD(MK, true, false); } \
   else { if (dres) PDT_BWD(MK, false, true); else PDT_BWD(MK, false, false); }
@@ -692,7 +701,8 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
 void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                                 const float* stats, const float* gamma, const float* sums, int mask,
                                 bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
-                                uint8_t* dy8, float* state, int slot, hipStream_t st) {
+                                uint8_t* dy8, float* state, int slot, hipStream_t st, float* dgamma,
+                                float* dbeta) {
   if (!training) throw std::runtime_error("bn_act_bwd_apply_q8: training mode only");
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
@@ -707,7 +717,7 @@ void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uin
   float invM = 1.f / (float)M;
 #define PDT_BWDQ(MK, DRS)                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, true, DRS, true>), g, blk, 0, st, DZ, Z, Y, stats, \
-                     gamma, sums, nvec, K8, invM, DY, DR, D8, state, slot)
+                     gamma, sums, nvec, K8, invM, DY, DR, D8, state, slot, dgamma, dbeta)
   if (mask == 1) { if (dres) PDT_BWDQ(1, true); else PDT_BWDQ(1, false); }
   else if (mask == 2) { if (dres) PDT_BWDQ(2, true); else PDT_BWDQ(2, false); }
   else { if (dres) PDT_BWDQ(0, true); else PDT_BWDQ(0, false); }

@@ -132,6 +132,7 @@ struct NtArgs {
                           // ReLU bitmask: one byte per 8-channel chunk, bit q = (z[c0 + q] > 0)
   const float* bn_stats;  // [4][Nout] mean, invstd, scale, shift
   float* bn_part;
+  float* bn_acc;  // non-null: fp32-atomic accumulation of the partials into [2][Nout] instead
   int bn_mask, bn_group0;
   // addend layout: 0 = same NHWC layout as out; 2 = compact stride-2 map addend[n][h/2][w/2] that
   // contributes only at even (h, w) -- the input gradient of a 1x1/s2 projection shortcut, which
@@ -702,9 +703,14 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
         S += red[(w * 2) * BN + t];
         Q += red[(w * 2 + 1) * BN + t];
       }
-      float* pp = P.bn_part + ((int64_t)(P.bn_group0 + tmi) * 2) * P.Nout + n0 + t;
-      pp[0] = S;
-      pp[P.Nout] = Q;
+      if (P.bn_acc != nullptr) {  // the BN-backward apply reads the finished sums: no reduce launch
+        unsafeAtomicAdd(P.bn_acc + n0 + t, S);
+        unsafeAtomicAdd(P.bn_acc + P.Nout + n0 + t, Q);
+      } else {
+        float* pp = P.bn_part + ((int64_t)(P.bn_group0 + tmi) * 2) * P.Nout + n0 + t;
+        pp[0] = S;
+        pp[P.Nout] = Q;
+      }
     }
   }
 }
@@ -1968,7 +1974,7 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       a.tr0 = r0; a.ts0 = s0; a.tstep = str;
       a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;
       if (bn != nullptr) {
-        a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part;
+        a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part; a.bn_acc = bn->acc;
         a.bn_mask = bn->mask; a.bn_group0 = group0;
         group0 += ceil_div(a.M, conv_nt_group_rows(a.M, a.Nout, a.Kg * EB));
         dispatch_nt<true, EPI_BNB, OP>(a, st);

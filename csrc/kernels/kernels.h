@@ -87,6 +87,7 @@ struct BnBwdFuse {
   const float* stats;    // [4][C] mean, invstd, scale, shift
   float* part;           // [G][2][C]
   int mask;
+  float* acc = nullptr;  // non-null: partials fp32-atomically summed into [2][C] (part unused)
 };
 int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes = 2);
 // addend_sub = 2: addend is a compact [N, ceil(H/2), ceil(W/2), C] map added at even (h, w) only
@@ -148,7 +149,9 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
 void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                              const float* stats, const float* gamma, const float* sums, int mask,
                              bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
-                             hipStream_t st);
+                             hipStream_t st, float* dgamma = nullptr, float* dbeta = nullptr);
+// dgamma/dbeta (optional): += sums[1]*invstd, += sums[0] (the BN parameter gradients, for sums
+// accumulated by the producing dgrad's epilogue atomics -- BnBwdFuse::acc)
 
 // Stem BN + ReLU + 3x3/s2/p1 max pool fused (bn_act.hip): out/idx as maxpool_fwd of the ReLU'd
 // bf16 z, which is never written.  Backward: the BN reduction / apply with dz gathered from the
@@ -262,7 +265,8 @@ void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* os
 void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,
                                 const float* stats, const float* gamma, const float* sums, int mask,
                                 bool training, int64_t M, int K, uint16_t* dy, uint16_t* dres,
-                                uint8_t* dy8, float* state, int slot, hipStream_t st);
+                                uint8_t* dy8, float* state, int slot, hipStream_t st,
+                                float* dgamma = nullptr, float* dbeta = nullptr);
 
 // ---------------------------------------------------------------- xgmi.hip
 // Direct one-hop all-reduce of elements [lo, lo + count) of every rank's fp32 gradient buffer

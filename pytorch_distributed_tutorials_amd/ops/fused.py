@@ -42,6 +42,22 @@ _FP8_WGRAD = os.environ.get("PDT_FP8_WGRAD", "1") != "0"
 # fp8-only storage: activations / input gradients whose every consumer reads the fp8 copy are not
 # written in bf16 at all (interior bottleneck outputs, and dy of convs with fp8 dgrad + fp8 wgrad)
 _FP8_ONLY = os.environ.get("PDT_FP8_ONLY", "1") != "0"
+# PDT_BN_ACC=1 (A/B knob, non-deterministic runs only): BN-backward sums of a BN-fused dgrad
+# accumulated by its epilogue's fp32 atomics into a per-BN [2, C] buffer -- no partial buffer and
+# no reduce launch on the main stream; the consuming apply adds the BN parameter gradients, and the
+# buffer is re-zeroed on the weight-gradient side stream once the apply is done.  Measured neutral
+# (r3t, one box: 18.949 / 18.944 ms off vs 18.925 / 18.983 on): the 47 reduce launches it removes
+# sat beside weight-gradient work that filled the GPU, so off (deterministic sums) by default.
+_BN_ACC = os.environ.get("PDT_BN_ACC", "0") == "1"
+
+
+def _bacc(p, c):
+    """The zeroed [2, C] fp32 BN-backward sum accumulator of BatchNorm weight ``p``."""
+    a = getattr(p, "_pdt_bacc", None)
+    if a is None or a.numel() != 2 * c or a.device != p.device:
+        a = torch.zeros(2, c, dtype=torch.float32, device=p.device)
+        p._pdt_bacc = a
+    return a
 _FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
 _COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
 
@@ -902,20 +918,24 @@ class _ResidualBlock(torch.autograd.Function):
         in8 = ctx.in8
         ctx.in8 = None
 
+        deferred = {}  # unit j -> (accumulator, dgamma sink, dbeta sink): BN sums from epilogue atomics
+
         def wgrad(j, dy_, xin_, st_, pd_, d8_=None, x8_=None):
             w_ = tensors[j]
             sink = _grad_sink(params[j])
+            dfr = deferred.pop(j, None)
+            zero = dfr[0] if dfr is not None else None  # its apply is queued: re-zero on the side stream
             k_, c_ = w_.shape[0], w_.shape[1]
             if (d8_ is not None and x8_ is not None and not det and c_ % 16 == 0 and k_ % 64 == 0
                     and x8_[0].shape[3] == c_):
                 # e5m2 dy x e4m3 x on the MX-rate MFMA, both already produced for the fp8 GEMMs
                 if sink is not None:
                     C.conv_wgrad_fp8(side.cuda_stream if side is not None else 0, d8_[0], x8_[0], d8_[1],
-                                     x8_[1], list(w_.shape), st_, pd_, sink)
+                                     x8_[1], list(w_.shape), st_, pd_, sink, zero)
                     sunk.append(params[j])
                 else:
                     grads[j] = C.conv_wgrad_fp8(0, d8_[0], x8_[0], d8_[1], x8_[1], list(w_.shape), st_,
-                                                pd_).to(w_.dtype)
+                                                pd_, None, zero).to(w_.dtype)
                 return
             if dy_ is None or xin_ is None:
                 raise RuntimeError("fp8-only operands reached the bf16 weight gradient")
@@ -923,12 +943,15 @@ class _ResidualBlock(torch.autograd.Function):
                 # weight gradient into the flat buffer on the side stream, concurrent with the
                 # dgrad chain; all-reduce and optimizer wait for that stream (streams.py)
                 if side is not None:  # one native call: stream hand-off, launch, record_stream
-                    C.conv_wgrad_side(side.cuda_stream, dy_, xin_, list(w_.shape), st_, pd_, det, sink)
+                    C.conv_wgrad_side(side.cuda_stream, dy_, xin_, list(w_.shape), st_, pd_, det, sink, zero)
+                    zero = None
                 else:
                     C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det, sink)
                 sunk.append(params[j])
             else:
                 grads[j] = C.conv_wgrad(dy_, xin_, list(w_.shape), st_, pd_, det).to(w_.dtype)
+            if zero is not None:
+                zero.zero_()
 
         def bnreduce(j, dz_, z_, y_, stt_, mask_):
             if z_ is None:  # fp8-only z: interior units recompute the ReLU mask from y (mask 2)
@@ -950,6 +973,8 @@ class _ResidualBlock(torch.autograd.Function):
             (K % 64 == 0 and the conv input's e4m3 copy x8_ exists)"""
             gamma_ = tensors[j + 1]
             k_ = dz_.shape[3]
+            dfr = deferred.get(j)
+            pg = (dfr[1], dfr[2]) if dfr is not None else (None, None)
             wgrad8 = (x8_ is not None and not det and k_ % 64 == 0 and tensors[j].shape[1] % 16 == 0
                       and x8_[0].shape[3] == tensors[j].shape[1])
             if ctx.fp8b and tr_ and ((need_dgrad and k_ % 128 == 0) or wgrad8):
@@ -958,10 +983,10 @@ class _ResidualBlock(torch.autograd.Function):
                 # fp8-only dy: the dgrad (if any) and the weight gradient both read the e5m2 copy
                 want_dy = not (_FP8_ONLY and wgrad8 and (not need_dgrad or k_ % 128 == 0))
                 dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_ if z_ is not None else y_, y_, stt_, gamma_,
-                                                       sums_, mask_, want_dres, stq.buf, slot, want_dy)
+                                                       sums_, mask_, want_dres, stq.buf, slot, want_dy, *pg)
                 return dy_, dres_, (q_, stq.deq(slot))
             dy_, dres_ = C.bn_act_bwd_apply(dz_, z_ if z_ is not None else y_, y_, stt_, gamma_, sums_, mask_,
-                                            tr_, want_dres)
+                                            tr_, want_dres, *pg)
             return dy_, dres_, None
 
         def dgrad(dy_, d8_, w_, xshape, st_, pd_, addend_):
@@ -970,18 +995,23 @@ class _ResidualBlock(torch.autograd.Function):
                 return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
             return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
 
-        def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None):
+        def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None, acc=None):
             if d8_ is not None and d8_[0].shape[3] % 128 == 0:
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
-                                           stt_, mask_, sg, sb)
+                                           stt_, mask_, sg, sb, acc)
             return C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb,
-                                   _packed_crsk(w_))
+                                   _packed_crsk(w_), acc)
 
         def dgrad_bn(j, dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_):
             """input gradient of a conv + BN backward reduction of unit j (its producer)"""
             sg, sb = _grad_sink(params[j + 1]), _grad_sink(params[j + 2])
-            if sg is not None and sb is not None:
+            if sg is not None and sb is not None and _BN_ACC and not det:
+                acc = _bacc(params[j + 1], stt_.shape[1])
+                g_, sums_ = dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, acc=acc)
+                deferred[j] = (acc, sg, sb)  # the apply of unit j adds dgamma / dbeta
+                sunk.extend([params[j + 1], params[j + 2]])
+            elif sg is not None and sb is not None:
                 g_, sums_ = dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb)
                 sunk.extend([params[j + 1], params[j + 2]])
             else:
@@ -1017,12 +1047,16 @@ class _ResidualBlock(torch.autograd.Function):
         pre = None
         ho = ctx.handoff_out
         if ho.deposit is not None:
-            g_dep, sums_dep = ho.deposit
+            g_dep, sums_dep, acc_dep = ho.deposit
             ho.deposit = None
             jl = 5 * (nch - 1)
             if g_dep.data_ptr() == dz.data_ptr() and g_dep.shape == dz.shape:
                 pre = (dz, sums_dep)
                 sunk.extend([params[jl + 1], params[jl + 2]])
+                if acc_dep is not None:  # atomic sums: this block's apply adds dgamma / dbeta
+                    deferred[jl] = (acc_dep, _grad_sink(params[jl + 1]), _grad_sink(params[jl + 2]))
+            elif acc_dep is not None:  # another consumer contributed: discard the unused sums
+                acc_dep.zero_()
             else:  # another consumer contributed: undo the deposited BN-parameter gradients
                 inv = units[nch - 1][2][1]
                 with torch.no_grad():
@@ -1081,12 +1115,20 @@ class _ResidualBlock(torch.autograd.Function):
                     if sg is not None and sb is not None and _BN_HANDOFF and _FUSE_DGRAD_BN:
                         # previous block's last unit: relu mask from its output z = x
                         zsrc, zmode = (hi.zmask, 3) if hi.zmask is not None else (x, 1)
-                        dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
-                                                   hi.stats, zmode, sg, sb)
-                        hi.deposit = (dz, sums_in)
+                        if _BN_ACC and not det:
+                            acc = _bacc(hi.gamma, hi.stats.shape[1])
+                            dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
+                                                       hi.stats, zmode, acc=acc)
+                            hi.deposit = (dz, sums_in, acc)
+                        else:
+                            dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
+                                                       hi.stats, zmode, sg, sb)
+                            hi.deposit = (dz, sums_in, None)
                     else:
                         dz = dgrad(dy, d8, w, list(x.shape), st, pd, addend)
         ctx.handoff_in = None
+        for acc_, _, _ in deferred.values():  # (every unit's weight gradient re-zeroes its own)
+            acc_.zero_()
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
         return (dz, None, None, None, *grads)
