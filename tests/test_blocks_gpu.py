@@ -39,11 +39,13 @@ def _rel(a, b):
 
 
 def _stage_cases():
-    # (arch, stage index, input channels, input spatial size)
-    return [("resnet50", 1, 64, 56), ("resnet50", 2, 256, 56), ("resnet50", 3, 512, 28),
-            ("resnet50", 4, 1024, 14),
-            ("resnet18", 1, 64, 56), ("resnet18", 2, 64, 56), ("resnet18", 3, 128, 28),
-            ("resnet18", 4, 256, 14)]
+    # (arch, stage index, input channels, input spatial size, atomic BN-backward sums)
+    return [("resnet50", 1, 64, 56, False), ("resnet50", 2, 256, 56, False), ("resnet50", 3, 512, 28, False),
+            ("resnet50", 4, 1024, 14, False),
+            ("resnet18", 1, 64, 56, False), ("resnet18", 2, 64, 56, False), ("resnet18", 3, 128, 28, False),
+            ("resnet18", 4, 256, 14, False),
+            # PDT_BN_ACC path: epilogue-atomic sums, dgamma/dbeta in the apply, side-stream re-zero
+            ("resnet50", 1, 64, 56, True), ("resnet50", 3, 512, 28, True)]
 
 
 @pytest.fixture(scope="module")
@@ -70,8 +72,10 @@ def models(gpu):
     return out
 
 
-@pytest.mark.parametrize("arch,stage,cin,hw", _stage_cases())
-def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw):
+@pytest.mark.parametrize("arch,stage,cin,hw,bn_acc", _stage_cases())
+def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc, monkeypatch):
+    import pytorch_distributed_tutorials_amd.ops.fused as fused
+    monkeypatch.setattr(fused, "_BN_ACC", bn_acc)
     ref_model, nat_model, ddp = models[arch]
     layer_r = getattr(ref_model, f"layer{stage}")
     layer_n = getattr(nat_model, f"layer{stage}")
