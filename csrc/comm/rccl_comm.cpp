@@ -2,9 +2,11 @@
 
 #include <c10/hip/HIPGuard.h>
 
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 
 namespace pdt {
@@ -43,6 +45,30 @@ static bool comm_high_priority() {
   return e && e[0] == '1';
 }
 
+// Communicator mode.  Default: a BLOCKING communicator whose init runs on a helper thread that
+// the constructor waits for with a deadline.  A non-blocking communicator (PDT_RCCL_NONBLOCKING=1)
+// makes every collective return ncclInProgress and the issuing thread -- the autograd thread, which
+// also issues the rest of the backward -- poll ncclCommGetAsyncError until RCCL's async enqueue
+// finishes.  A/B on MI355X with the world-1 forced reducer showed no step-time difference
+// (r3w: 28.47 vs 28.52 ms, both then dominated by the stream-priority effect described in
+// ops/streams.py), so the default is the one whose collectives need no host polling.
+static bool rccl_nonblocking() {
+  const char* e = std::getenv("PDT_RCCL_NONBLOCKING");
+  return e && e[0] == '1';
+}
+
+namespace {
+// Shared between the constructor and the init thread: the thread outlives a timed-out constructor
+// (it stays blocked inside ncclCommInitRankConfig until its peers arrive or the process exits).
+struct InitJob {
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  ncclResult_t r = ncclInProgress;
+  ncclComm_t comm = nullptr;
+};
+}  // namespace
+
 RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, const RcclOptions& opt)
     : rank_(rank), world_(world), device_(device), opt_(opt),
       stream_(c10::hip::getStreamFromPool(comm_high_priority(), (c10::DeviceIndex)device)) {
@@ -50,29 +76,50 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, cons
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   ncclUniqueId id;
   memcpy(id.internal, uid.data(), sizeof(id.internal));
-  // Non-blocking init polled against a deadline (ProcessGroupNCCL's init timeout): a blocking
+  // Init is bounded by a deadline (ProcessGroupNCCL's init timeout): an unbounded
   // ncclCommInitRank whose peer never arrives would hang this rank forever.
+  nonblocking_ = rccl_nonblocking();
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
+  cfg.blocking = nonblocking_ ? 0 : 1;
   if (opt_.min_channels > 0) cfg.minCTAs = opt_.min_channels;
   if (opt_.max_channels > 0) cfg.maxCTAs = opt_.max_channels;
   const auto t0 = std::chrono::steady_clock::now();
-  ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (comm_) ncclCommAbort(comm_);
-    comm_ = nullptr;
-    rccl_check(r, "ncclCommInitRankConfig");
-  }
   ncclResult_t st = ncclInProgress;
-  while (true) {
-    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
-    if (st != ncclInProgress) break;
-    if (since(t0) > opt_.init_timeout_s) break;
-    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  if (nonblocking_) {
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      rccl_check(r, "ncclCommInitRankConfig");
+    }
+    while (true) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      if (st != ncclInProgress) break;
+      if (since(t0) > opt_.init_timeout_s) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  } else {
+    auto job = std::make_shared<InitJob>();
+    std::thread([job, id, world, rank, device, cfg]() mutable {
+      ncclComm_t c = nullptr;
+      ncclResult_t r = ncclInvalidUsage;
+      if (hipSetDevice(device) == hipSuccess) r = ncclCommInitRankConfig(&c, world, id, rank, &cfg);
+      std::lock_guard<std::mutex> lk(job->m);
+      job->comm = c;
+      job->r = r;
+      job->done = true;
+      job->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->m);
+    const auto limit = std::chrono::duration<double>(opt_.init_timeout_s);
+    if (job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+      st = job->r;
+      comm_ = job->comm;
+    }  // else: still in progress; the detached thread keeps the half-built communicator
   }
   init_s_ = since(t0);
   if (st != ncclSuccess) {
-    ncclCommAbort(comm_);
+    if (comm_) ncclCommAbort(comm_);
     comm_ = nullptr;
     char buf[512];
     if (st == ncclInProgress)
@@ -94,7 +141,16 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, cons
 RcclComm::~RcclComm() {
   stop_.store(true);
   if (monitor_.joinable()) monitor_.join();
-  if (comm_ && !aborted_.load()) {
+  if (comm_ && !aborted_.load() && !nonblocking_) {
+    // blocking communicator: destroy only once the comm stream has drained (bounded wait); a
+    // collective stuck on a dead peer is aborted instead of blocking our exit
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipStreamQuery(stream())) == hipErrorNotReady && since(t0) < 10.0)
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (q == hipSuccess) ncclCommDestroy(comm_);
+    else ncclCommAbort(comm_);
+  } else if (comm_ && !aborted_.load()) {
     // non-blocking communicator: finalize (flushes outstanding work) must complete before
     // destroy; a peer that died mid-teardown must not hang our exit, so the wait is bounded
     ncclResult_t r = ncclCommFinalize(comm_);

@@ -5,9 +5,11 @@
 // handling: a watchdog thread, async-error checks and a 10-minute collective timeout.  Here the
 // data-parallel hot path talks to RCCL directly, so this class carries that failure handling too:
 //
-//  * init is NON-BLOCKING (ncclCommInitRankConfig, blocking = 0) and polled against a deadline:
-//    a peer that never joins makes init throw a clear error after `init_timeout_s` instead of
-//    blocking forever inside ncclCommInitRank;
+//  * init is bounded by a deadline: ncclCommInitRankConfig runs on a helper thread the
+//    constructor waits for, so a peer that never joins makes init throw a clear error after
+//    `init_timeout_s` instead of blocking forever.  The communicator itself is BLOCKING:
+//    a non-blocking one (PDT_RCCL_NONBLOCKING=1, blocking = 0) makes every collective's issuing
+//    thread poll for the async enqueue;
 //  * a monitor thread polls ncclCommGetAsyncError and the completion event of every enqueued
 //    collective; an async error or a collective older than `op_timeout_s` aborts the
 //    communicator (ncclCommAbort unblocks kernels waiting on a dead peer), records the error --
@@ -100,6 +102,7 @@ class RcclComm {
   hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr;
   at::Tensor barrier_buf_;
   double init_s_ = 0.0;
+  bool nonblocking_ = false;  // PDT_RCCL_NONBLOCKING=1: ncclConfig_t.blocking = 0
 
   struct Pending {
     hipEvent_t ev;

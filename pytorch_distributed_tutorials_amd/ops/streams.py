@@ -58,9 +58,8 @@ def critical_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     when both have workgroups waiting the dispatcher hands CUs to the critical path first and the
     side work fills what is left.  Measured on MI355X, ResNet-50 b256 (r3l, same box): 20.01 ->
     19.56 ms/step.  (Confining the weight-gradient stream to a CU mask instead -- 128 or 192 of
-    256 CUs, ``C.cu_masked_stream`` -- was 28 ms/step.)  ``PDT_MAIN_PRIO=0`` keeps the default
-    stream."""
-    if device.type != "cuda" or os.environ.get("PDT_MAIN_PRIO", "1") == "0":
+    256 CUs, ``C.cu_masked_stream`` -- was 28 ms/step.)"""
+    if device.type != "cuda":
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _critical.get(idx)
@@ -71,9 +70,29 @@ def critical_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     return s
 
 
-def use_critical_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
-    """Make :func:`critical_stream` the current stream of ``device`` (call once, before the model
-    and its buffers are touched, so every later op orders on it)."""
+def critical_priority_wanted(collective: bool, graph: bool) -> bool:
+    """Whether the step should run on :func:`critical_stream`.
+
+    Only for an eager step with no gradient collectives.  The priority pays in the plain
+    single-GPU step (r3z, same box: 19.41 -> 18.95 ms) but costs far more than it gains as soon
+    as the step adds cross-stream synchronisation with a normal-priority stream outside the
+    compute chain: ResNet-50 with the gradient reducer (world-1 RCCL or xGMI) 19.5 -> 28.4 ms,
+    its HIP-graph replay 20.7 -> 29.6 ms, ResNet-18/CIFAR graph replay 2.04 -> 6.34 ms; every
+    small main-stream kernel is ~35 us longer in the kernel trace
+    (``profiles/r3z_priority_vs_sync.md``).  ``PDT_MAIN_PRIO=1`` / ``=0`` forces it on / off."""
+    e = os.environ.get("PDT_MAIN_PRIO", "auto")
+    if e in ("0", "1"):
+        return e == "1"
+    return not collective and not graph
+
+
+def use_critical_stream(device: torch.device, collective: bool = False,
+                        graph: bool = False) -> Optional[torch.cuda.Stream]:
+    """Make :func:`critical_stream` the current stream of ``device`` when
+    :func:`critical_priority_wanted` says so (call once, before the model and its buffers are
+    touched, so every later op orders on it)."""
+    if not critical_priority_wanted(collective, graph):
+        return None
     s = critical_stream(device)
     if s is not None:
         torch.cuda.set_stream(s)

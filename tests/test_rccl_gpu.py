@@ -158,8 +158,9 @@ def _py(code, timeout=120, **env_extra):
 
 
 def test_rccl_init_times_out_when_peer_never_joins(gpu):
-    # rank 0 of a 2-rank communicator whose rank 1 never calls init: the non-blocking init must
-    # give up at its deadline with a clear error (a blocking ncclCommInitRank would wait forever)
+    # rank 0 of a 2-rank communicator whose rank 1 never calls init: the deadline-bounded init
+    # (helper-thread init of a blocking communicator, or PDT_RCCL_NONBLOCKING=1 polling) must give
+    # up at its deadline with a clear error (a bare ncclCommInitRank would wait forever)
     code = (
         "import time, torch\n"
         "from pytorch_distributed_tutorials_amd.ops import _ext\n"
