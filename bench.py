@@ -57,6 +57,8 @@ def parse(argv=None):
     p.add_argument("--force-comm", action="store_true",
                    help="native impl: run the RCCL communicator + C++ reducer + buffer broadcasts "
                         "even at N=1 (world-1 RCCL communicator; exercises the multi-GPU path)")
+    p.add_argument("--no-broadcast-buffers", action="store_true",
+                   help="DDP broadcast_buffers=False: BatchNorm running stats stay per-rank")
     p.add_argument("--comm-timing", action="store_true",
                    help="record all-reduce time / exposed tail per step (native RCCL path)")
     p.add_argument("--deterministic", action="store_true",
@@ -164,7 +166,8 @@ def main(argv=None) -> int:
                                       bucket_cap_mb=args.bucket_mb, wire_dtype=args.wire_dtype,
                                       first_bucket_mb=args.first_bucket_mb,
                                       last_bucket_mb=args.last_bucket_mb,
-                                      force_reducer=args.force_comm, comm_options=copts, comm=args.comm)
+                                      force_reducer=args.force_comm, comm_options=copts, comm=args.comm,
+                                      broadcast_buffers=not args.no_broadcast_buffers)
         holder["ddp"] = ddp
         if args.comm_timing:
             ddp.enable_comm_timing(True)

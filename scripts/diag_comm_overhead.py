@@ -30,6 +30,30 @@ def chain(x, n, ev=None):
     return (time.perf_counter() - t0) * 1e6 / n
 
 
+def cross(n, prio_main, back, every=10):
+    """Tiny kernels on a `main` stream (high priority if prio_main); every `every` kernels the
+    normal-priority `other` stream waits for main and runs one kernel, and (back) main waits for
+    other again -- the reducer's comm_wait_current / current_wait_comm pattern."""
+    lo, hi = torch.cuda.Stream.priority_range()
+    main = torch.cuda.Stream(priority=min(lo, hi) if prio_main else 0)
+    other = torch.cuda.Stream()
+    x = torch.zeros(1024, device="cuda")
+    y = torch.zeros(1024, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n):
+        with torch.cuda.stream(main):
+            x.add_(1.0)
+        if i % every == every - 1:
+            other.wait_stream(main)
+            with torch.cuda.stream(other):
+                y.add_(1.0)
+            if back:
+                main.wait_stream(other)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e6 / n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2000)
@@ -52,6 +76,9 @@ def main():
     out["after_sleep_us"] = chain(x, a.n)
     del comm
     out["after_destroy_us"] = chain(x, a.n)
+    for prio in (False, True):
+        for back in (False, True):
+            out[f"cross_prio{int(prio)}_back{int(back)}_us"] = cross(a.n, prio, back)
     print(json.dumps({k: round(v, 2) for k, v in out.items()}))
 
 
