@@ -302,7 +302,14 @@ def main(argv=None) -> int:
     if watchdog is not None:
         watchdog.stop()
     if world > 1:
+        barrier()
         dist.destroy_process_group()
+        # every rank is past its last collective: end the process here rather than in interpreter
+        # teardown, where the native communicator's destructor would run in an unspecified order
+        # with torch's (a late peer must not be able to hold a finished rank at exit)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     return 0
 
 
