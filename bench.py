@@ -194,6 +194,10 @@ def main(argv=None) -> int:
     if args.impl == "torch":
         images = images.contiguous(memory_format=torch.channels_last)
 
+    diag_blocked = None
+    if os.environ.get("PDT_DIAG_BLOCKED") == "1" and dev.type == "cuda":
+        diag_blocked = (torch.cuda.Stream(), torch.zeros(16, device=dev))
+
     def step():
         opt.zero_grad()
         if autocast is not None:
@@ -203,6 +207,12 @@ def main(argv=None) -> int:
         else:
             out = ddp(images)
             loss = criterion(out, labels)
+        if diag_blocked is not None:  # PDT_DIAG_BLOCKED: a side queue parked on a barrier
+            ev = torch.cuda.Event()
+            ev.record()
+            diag_blocked[0].wait_event(ev)
+            with torch.cuda.stream(diag_blocked[0]):
+                diag_blocked[1].add_(1.0)
         loss.backward()
         opt.step()
         return loss

@@ -243,7 +243,18 @@ void RcclComm::monitor_loop() {
   }
 }
 
+// A/B knob (PDT_RCCL_TRACK=0): no per-collective completion event, so the monitor sees only
+// asynchronous RCCL errors (no collective timeout)
+static bool rccl_track() {
+  static const bool on = [] {
+    const char* e = std::getenv("PDT_RCCL_TRACK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void RcclComm::track(const char* what) {
+  if (!rccl_track()) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream(), &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
     return;  // captured collectives run at replay; the process watchdog covers graph mode
