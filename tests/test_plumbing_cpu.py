@@ -310,3 +310,19 @@ def test_auto_last_bucket_cap_from_tail_model():
         capped = [sum(sizes[i] for i in b) for b in ddp_bucket_plan(sizes, last_bucket_mb=cap)]
         assert capped[-1] <= cap * 2**20 and sum(capped) == sum(base)
         assert tail_time_us(capped, world, 7) < tail_time_us(base, world, 7)
+
+
+def test_critical_priority_policy(monkeypatch):
+    """High-priority critical stream only for an eager step without gradient collectives
+    (profiles/r3z_priority_vs_sync.md); PDT_MAIN_PRIO forces it either way."""
+    from pytorch_distributed_tutorials_amd.ops import streams
+    monkeypatch.delenv("PDT_MAIN_PRIO", raising=False)
+    assert streams.critical_priority_wanted(collective=False, graph=False)
+    assert not streams.critical_priority_wanted(collective=True, graph=False)
+    assert not streams.critical_priority_wanted(collective=False, graph=True)
+    monkeypatch.setenv("PDT_MAIN_PRIO", "0")
+    assert not streams.critical_priority_wanted(collective=False, graph=False)
+    monkeypatch.setenv("PDT_MAIN_PRIO", "1")
+    assert streams.critical_priority_wanted(collective=True, graph=True)
+    # CPU device: nothing to make current
+    assert streams.use_critical_stream(torch.device("cpu")) is None
