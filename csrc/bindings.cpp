@@ -313,7 +313,8 @@ pdt::ConvShape fp8_dgrad_shape(const Tensor& dy8, const Tensor& wt8, const Tenso
               "ascale must be a device fp32 scalar");
   auto s = shape_of(xs[0], xs[1], xs[2], xs[3], wt8.size(3), wt8.size(1), wt8.size(2), stride, pad);
   TORCH_CHECK(s.Ho == dy8.size(1) && s.Wo == dy8.size(2) && s.K == dy8.size(3), "dgrad: dy shape mismatch");
-  TORCH_CHECK(s.K % 128 == 0, "fp8 dgrad: output channels must be a multiple of 128");
+  TORCH_CHECK(s.K % 128 == 0 || (s.K % 16 == 0 && s.stride == 1),
+              "fp8 dgrad: output channels must be a multiple of 128 (or of 16 at stride 1)");
   return s;
 }
 

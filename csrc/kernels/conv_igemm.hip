@@ -874,7 +874,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
         const int ch = kk - tap * P.CA;
         const int r = (int)fdiv((uint32_t)tap, P.div_s);
         const int s = tap - r * P.S;
-        int h = a_h0[i] + r, w = a_w0[i] + s;
+        // tap (r, s) reads A at (dr0 + r*dstep, ds0 + s*dstep): forward (0, +1) or a stride-1
+        // dgrad (pad, -1)
+        int h = a_h0[i] + P.dr0 + r * P.dstep, w = a_w0[i] + P.ds0 + s * P.dstep;
         bool ok = kk < P.Kg && (unsigned)h < (unsigned)P.HA && (unsigned)w < (unsigned)P.WA;
         uint32_t off = ok ? (uint32_t)(((a_pix[i] + h * P.WA + w) * P.CA + ch) * EB) : OOB;
         glds16(ra, As + (wid * A_PW + i) * 1024, off);
@@ -1937,9 +1939,14 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
                             const BnBwdFuse* bn, int addend_sub) {
   if (addend_sub != 0 && addend_sub != 2) throw std::runtime_error("conv_dgrad: addend_sub must be 0 or 2");
   constexpr int EB = OP == OP_BF16 ? 2 : 1;
-  if (s.K % (128 / EB) != 0)
-    throw std::runtime_error("conv_dgrad: output channels must fill 128-byte rows (64 bf16 / 128 fp8)");
   const int str = s.stride;
+  // full: dy rows are whole 128-byte K-steps per tap (the C64 loader, any stride).  fp8 with
+  // K % 16 == 0 otherwise (the 64-channel layer-1 convs): the generic loader packs K-steps across
+  // taps; its tap walk covers stride 1 only (one parity class, all R x S taps).
+  const bool full = s.K % (128 / EB) == 0;
+  if (!full && (OP == OP_BF16 || s.K % 16 != 0 || str != 1))
+    throw std::runtime_error("conv_dgrad: output channels must fill 128-byte rows (64 bf16 / 128 fp8), "
+                             "or be a multiple of 16 for a stride-1 fp8 dgrad");
   int group0 = 0;
   for (int ph = 0; ph < str; ++ph)
     for (int pw = 0; pw < str; ++pw) {
@@ -1977,8 +1984,14 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
         a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part; a.bn_acc = bn->acc;
         a.bn_mask = bn->mask; a.bn_group0 = group0;
         group0 += ceil_div(a.M, conv_nt_group_rows(a.M, a.Nout, a.Kg * EB));
+        if constexpr (OP != OP_BF16) {
+          if (!full) { dispatch_nt<false, EPI_BNB, OP>(a, st); continue; }
+        }
         dispatch_nt<true, EPI_BNB, OP>(a, st);
       } else {
+        if constexpr (OP != OP_BF16) {
+          if (!full) { dispatch_nt<false, EPI_PLAIN, OP>(a, st); continue; }
+        }
         dispatch_nt<true, EPI_PLAIN, OP>(a, st);
       }
     }

@@ -751,6 +751,16 @@ def _fp8_conv_ok(r, s, cx):
     return r * s * cx >= _FP8_KMIN
 
 
+_FP8_DGRAD_NARROW = os.environ.get("PDT_FP8_DGRAD_NARROW", "1") != "0"
+
+
+def _fp8_dgrad_ok(k, stride):
+    """fp8 input gradient for a dy of k channels: whole 128-byte K-steps per tap (k % 128), or
+    (PDT_FP8_DGRAD_NARROW, default on) any k % 16 at stride 1 -- the 64-channel layer-1 convs, whose
+    dy then needs no bf16 copy at all when the weight gradient is fp8 too."""
+    return k % 128 == 0 or (_FP8_DGRAD_NARROW and stride == 1 and k % 16 == 0)
+
+
 def _fp8_only_ok(w_next, k, tr):
     """May unit output z (k channels, training) skip its bf16 copy?  Only when every reader takes the
     e4m3 copy: the next conv's forward GEMM and its fp8 weight gradient (backward masks of interior
@@ -967,21 +977,22 @@ class _ResidualBlock(torch.autograd.Function):
                 grads[j + 2] = sums_[0]
             return sums_
 
-        def apply(j, dz_, z_, y_, stt_, sums_, mask_, tr_, want_dres, need_dgrad, x8_=None):
+        def apply(j, dz_, z_, y_, stt_, sums_, mask_, tr_, want_dres, need_dgrad, x8_=None, stride_=0):
             """BN backward apply of unit j -> (dy, dres, d8); d8 = (e5m2 dy, its dequant factor)
-            when the dgrad consuming dy runs on fp8 (K % 128 == 0), or the weight gradient does
-            (K % 64 == 0 and the conv input's e4m3 copy x8_ exists)"""
+            when the dgrad consuming dy runs on fp8 (_fp8_dgrad_ok for the conv's stride), or the
+            weight gradient does (K % 64 == 0 and the conv input's e4m3 copy x8_ exists)"""
             gamma_ = tensors[j + 1]
             k_ = dz_.shape[3]
             dfr = deferred.get(j)
             pg = (dfr[1], dfr[2]) if dfr is not None else (None, None)
             wgrad8 = (x8_ is not None and not det and k_ % 64 == 0 and tensors[j].shape[1] % 16 == 0
                       and x8_[0].shape[3] == tensors[j].shape[1])
-            if ctx.fp8b and tr_ and ((need_dgrad and k_ % 128 == 0) or wgrad8):
+            dgrad8 = _fp8_dgrad_ok(k_, stride_)
+            if ctx.fp8b and tr_ and ((need_dgrad and dgrad8) or wgrad8):
                 stq = _q8_state(params[j + 1], dz_.device, "_pdt_q8b")
                 slot = stq.next_slot()
                 # fp8-only dy: the dgrad (if any) and the weight gradient both read the e5m2 copy
-                want_dy = not (_FP8_ONLY and wgrad8 and (not need_dgrad or k_ % 128 == 0))
+                want_dy = not (_FP8_ONLY and wgrad8 and (not need_dgrad or dgrad8))
                 dy_, dres_, q_ = C.bn_act_bwd_apply_q8(dz_, z_ if z_ is not None else y_, y_, stt_, gamma_,
                                                        sums_, mask_, want_dres, stq.buf, slot, want_dy, *pg)
                 return dy_, dres_, (q_, stq.deq(slot))
@@ -990,13 +1001,13 @@ class _ResidualBlock(torch.autograd.Function):
             return dy_, dres_, None
 
         def dgrad(dy_, d8_, w_, xshape, st_, pd_, addend_):
-            if d8_ is not None and d8_[0].shape[3] % 128 == 0:  # a 64-channel dy8 feeds only its wgrad
+            if d8_ is not None and _fp8_dgrad_ok(d8_[0].shape[3], st_):
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
             return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
 
         def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None, acc=None):
-            if d8_ is not None and d8_[0].shape[3] % 128 == 0:
+            if d8_ is not None and _fp8_dgrad_ok(d8_[0].shape[3], st_):
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
                                            stt_, mask_, sg, sb, acc)
@@ -1027,7 +1038,7 @@ class _ResidualBlock(torch.autograd.Function):
             wds = tensors[5 * nch]
             sums_ds = bnreduce(5 * nch, g_short_, g_short_, y_ds, st_ds, 0)
             dy_ds, _, d8_ds = apply(5 * nch, g_short_, g_short_, y_ds, st_ds, sums_ds, 0, tr2, False,
-                                    ctx.needs_input_grad[0], in8[0] if in8 else None)
+                                    ctx.needs_input_grad[0], in8[0] if in8 else None, st2)
             wgrad(5 * nch, dy_ds, x, st2, pd2, d8_ds, in8[0] if in8 else None)
             if not ctx.needs_input_grad[0]:
                 return None
@@ -1075,10 +1086,11 @@ class _ResidualBlock(torch.autograd.Function):
             if pre is None:
                 mask = 1 if last else 2  # inner units: ReLU mask recomputed from y, z never read
                 sums = bnreduce(5 * i, dz, z, y, stt, mask)
-                dy, dres, d8 = apply(5 * i, dz, z, y, stt, sums, mask, tr, last, need_dx, in8[i] if in8 else None)
+                dy, dres, d8 = apply(5 * i, dz, z, y, stt, sums, mask, tr, last, need_dx, in8[i] if in8 else None,
+                                     st)
             else:
                 g, sums = pre  # g = dz * relu'(unit i), reduced in the producing epilogue
-                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None)
+                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None, st)
                 dres = g
             pre = None
             wgrad(5 * i, dy, xin, st, pd, d8, in8[i] if in8 else None)

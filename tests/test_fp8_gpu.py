@@ -236,6 +236,10 @@ FP8_DGRAD_SHAPES = [
     (2, 15, 15, 128, 256, 3, 3, 2, 1),
     (4, 28, 28, 512, 128, 1, 1, 1, 0),
     (2, 16, 16, 512, 1024, 1, 1, 2, 0),
+    # K % 128 != 0 at stride 1 (the 64-channel layer-1 convs): generic loader, K-steps across taps
+    (2, 14, 14, 64, 64, 3, 3, 1, 1),
+    (3, 9, 9, 256, 64, 1, 1, 1, 0),
+    (2, 8, 8, 64, 80, 3, 3, 1, 1),
 ]
 
 
@@ -271,9 +275,9 @@ def test_conv_dgrad_fp8(gpu, native_ext, shape):
 
 
 @pytest.mark.parametrize("mask", [1, 2])
-def test_conv_dgrad_bn_fp8_matches_bf16_on_dequantized(gpu, native_ext, mask):
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 3, 1, 1), (2, 14, 14, 64, 64, 3, 3, 1, 1)])
+def test_conv_dgrad_bn_fp8_matches_bf16_on_dequantized(gpu, native_ext, mask, shape):
     C = native_ext
-    shape = (2, 14, 14, 256, 256, 3, 3, 1, 1)
     n, h, w_, c, k, r, s, st, pd = shape
     dy, w, dy8, ascale, wt8, wsc, dyd, wd = _dgrad_operands(C, shape, gpu, seed=12)
     g = torch.Generator().manual_seed(13)
