@@ -201,6 +201,26 @@ __device__ __forceinline__ int swz64_g(int row) { return (-(row >> 2)) & 3; }
 __device__ __forceinline__ int swz64(int row, int chunk) {
   return row * 64 + ((chunk ^ swz64_g(row)) << 4);
 }
+// Epilogue staging image of a wave's (TM*16) x (TN*16) bf16 tile, rows of TN*32 bytes.  Writes
+// are 8 B per lane (rows fr = lane & 15, one 16-B chunk per 32-lane half); reads are 16 B per lane
+// over CH_PER_ROW consecutive chunks of consecutive rows, serviced in the non-contiguous lane
+// groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (+32).  XOR of the chunk index with row & 15
+// (256-B rows) or (row >> 1) & 7 (128-B rows) puts both patterns on 16 distinct 16-B slots; the
+// old +16 B row pad was conflict-free for the writes only.  PDT_EPI_SWZ=0 builds the padded image.
+#ifndef PDT_EPI_SWZ
+#define PDT_EPI_SWZ 1
+#endif
+template <int TN>
+__device__ __forceinline__ int epi_off(int row, int chunk) {
+  static_assert(TN == 4 || TN == 8, "epilogue staging image: 128- or 256-byte rows");
+#if PDT_EPI_SWZ
+  if constexpr (TN == 8) return row * 256 + ((chunk ^ (row & 15)) << 4);
+  else return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+#else
+  return row * (TN * 32 + 16) + (chunk << 4);
+#endif
+}
+
 template <bool K32>
 __device__ __forceinline__ int swz_row(int row, int chunk) {
   if constexpr (K32) return swz64(row, chunk);
@@ -224,7 +244,8 @@ struct NtCfg {
   static_assert(A_PW * RPI * WAVES == BM && B_PW * RPI * WAVES == BN, "tile rows must split over waves");
   static constexpr int STAGE_BYTES = (BM + BN) * ROWB;
   static constexpr int PIPE_BYTES = STAGES * STAGE_BYTES;
-  static constexpr int EPI_PITCH = TN * 16 * 2 + 16;  // bytes per epilogue staging row (pixel)
+  // bytes per epilogue staging row (pixel): unpadded with the XOR image (epi_off), else +16 B pad
+  static constexpr int EPI_PITCH = TN * 16 * 2 + (PDT_EPI_SWZ ? 0 : 16);
   static constexpr int EPI_BYTES = WAVES * (TM * 16) * EPI_PITCH;
   static constexpr int SMEM = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
 };
@@ -412,7 +433,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
       uint2 v;
       v.x = pack2bf(acc[i][j][0], acc[i][j][1]);
       v.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(ep + (i * 16 + fr) * CFG::EPI_PITCH + (j * 16 + fq * 4) * 2) = v;
+      *reinterpret_cast<uint2*>(ep + epi_off<TN>(i * 16 + fr, j * 2 + (fq >> 1)) + (fq & 1) * 8) = v;
     }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): region is wave-private, no barrier needed
   __builtin_amdgcn_wave_barrier();
@@ -536,7 +557,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
       for (int it = 0; it < IT; ++it) {
         const int qd = lane + (b0 + it) * 64;
         const int r = qd / CH_PER_ROW, c = qd - r * CH_PER_ROW;
-        v4i v = *reinterpret_cast<const v4i*>(ep + r * CFG::EPI_PITCH + c * 16);
+        v4i v = *reinterpret_cast<const v4i*>(ep + epi_off<TN>(r, c));
         if constexpr (HA) {  // fused residual-gradient sum (block input of a residual block)
           f8 a = unpack8(__builtin_bit_cast(uint4, v));
           const f8 b = unpack8(__builtin_bit_cast(uint4, av[it]));
