@@ -747,7 +747,9 @@ _FP8_KMIN = int(os.environ.get("PDT_FP8_KMIN", "128"))
 def _fp8_conv_ok(r, s, cx):
     """fp8 forward conv for a GEMM K of r*s*cx >= PDT_FP8_KMIN (K = 64 half-fills the 128-wide fp8
     K-step).  128 (layer2's 1x1 over 128 channels on fp8, so its input needs no bf16 copy) vs 256:
-    fp8 b512 31.23 vs 31.39 ms, b256 17.04 vs 17.01 ms (r3p, one box)."""
+    fp8 b512 31.23 vs 31.39 ms, b256 17.04 vs 17.01 ms (r3p, one box).  64 (every layer-1 1x1 on
+    fp8 too, after the narrow fp8 dgrad) vs 128: b256 16.88 vs 16.77 ms, b512 31.09 vs 30.83 ms
+    (r3ap, one box)."""
     return r * s * cx >= _FP8_KMIN
 
 
