@@ -326,3 +326,15 @@ def test_critical_priority_policy(monkeypatch):
     assert streams.critical_priority_wanted(collective=True, graph=True)
     # CPU device: nothing to make current
     assert streams.use_critical_stream(torch.device("cpu")) is None
+
+
+def test_fp8_dgrad_policy(monkeypatch):
+    """fp8 input gradient: whole 128-byte K-steps per tap, or any 16-multiple at stride 1
+    (the generic loader's dgrad tap walk covers one parity class only)."""
+    from pytorch_distributed_tutorials_amd.ops import fused
+    monkeypatch.setattr(fused, "_FP8_DGRAD_NARROW", True)
+    assert fused._fp8_dgrad_ok(256, 2) and fused._fp8_dgrad_ok(128, 1)
+    assert fused._fp8_dgrad_ok(64, 1) and fused._fp8_dgrad_ok(80, 1)
+    assert not fused._fp8_dgrad_ok(64, 2) and not fused._fp8_dgrad_ok(72, 1)
+    monkeypatch.setattr(fused, "_FP8_DGRAD_NARROW", False)
+    assert not fused._fp8_dgrad_ok(64, 1) and fused._fp8_dgrad_ok(128, 1)
