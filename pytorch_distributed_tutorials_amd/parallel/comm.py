@@ -16,8 +16,8 @@ protocol over the rendezvous store, so that no rank ever enters the RCCL init al
    never answers makes the others raise a clear "peer never reached setup" error after the
    timeout; a rank that answers "cannot" makes EVERY rank take the same decision (fall back to
    ``torch.distributed`` collectives, or raise with ``comm='rccl'``).
-2. **init**: only when all ranks said yes, each one initialises its communicator non-blocking
-   with a deadline (``RcclComm(init_timeout=...)``): a peer that dies between the two phases
+2. **init**: only when all ranks said yes, each one initialises its communicator with a
+   deadline (``RcclComm(init_timeout=...)``; the init runs on a helper thread): a peer that dies between the two phases
    turns into an init-timeout error instead of a hang.
 
 After init a monitor thread in the communicator watches RCCL's async error state and the
@@ -88,7 +88,7 @@ def backend_name(pg=None) -> str:
 class CommOptions:
     """Failure handling and RCCL knobs of the native communicator.
 
-    ``init_timeout`` bounds both the cross-rank agreement and the non-blocking RCCL init;
+    ``init_timeout`` bounds both the cross-rank agreement and the RCCL init;
     ``op_timeout`` bounds each collective (0 = off).  ``exit_on_error`` ends the process when the
     monitor aborts the communicator (default: on when world > 1).  ``min_channels`` /
     ``max_channels`` bound the RCCL channels (rings) a collective spreads over (``ncclConfig_t``

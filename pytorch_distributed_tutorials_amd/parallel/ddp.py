@@ -218,7 +218,7 @@ class DistributedDataParallel(nn.Module):
         # ---- communicator
         # Every rank takes the same path -- native RCCL on all ranks or on none -- and no rank
         # enters the RCCL init unless all agreed to (parallel/comm.py: agreement through the
-        # store with a deadline, then a non-blocking init with a deadline).  A rank that cannot
+        # store with a deadline, then an RCCL init bounded by a deadline).  A rank that cannot
         # build it makes all ranks fall back (comm='auto') or all raise (comm='rccl'); a rank
         # that never shows up makes the others raise after the timeout instead of hanging.
         self.comm = None
