@@ -17,8 +17,8 @@ protocol over the rendezvous store, so that no rank ever enters the RCCL init al
    timeout; a rank that answers "cannot" makes EVERY rank take the same decision (fall back to
    ``torch.distributed`` collectives, or raise with ``comm='rccl'``).
 2. **init**: only when all ranks said yes, each one initialises its communicator with a
-   deadline (``RcclComm(init_timeout=...)``; the init runs on a helper thread): a peer that dies between the two phases
-   turns into an init-timeout error instead of a hang.
+   deadline (``RcclComm(init_timeout=...)``; the init runs on a helper thread): a peer that
+   dies between the two phases turns into an init-timeout error instead of a hang.
 
 After init a monitor thread in the communicator watches RCCL's async error state and the
 completion of every collective (``op_timeout``, ProcessGroupNCCL's 10-minute default), aborts the
