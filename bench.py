@@ -269,8 +269,22 @@ def main(argv=None) -> int:
         info = ddp.bucket_info()
         comm = {"native_comm": info["native_comm"], "reducer": info["reducer"], "xgmi": info["xgmi"],
                 "buckets_mb": [round(b / 2**20, 2) for b in info["bucket_bytes"]]}
-        if args.comm_timing:
-            comm["last_step"] = ddp.comm_stats()
+        # diagnostics for the scaling run (untimed, after the timed region): what the communicator
+        # reports about itself, and one step's all-reduce time / exposed tail from the reducer's
+        # HIP events (time from the first bucket's launch to the last bucket's end on the comm
+        # stream; exposed = the part after the backward's last kernel)
+        comm.update(ddp.comm_diagnostics())
+        if not args.comm_timing and not args.graph and ddp.enable_comm_timing(True):
+            step()
+            barrier()
+        st = ddp.comm_stats()
+        if st is not None:
+            comm["comm_ms"] = round(st["comm_ms"], 3)
+            comm["exposed_ms"] = round(st["exposed_ms"], 3)
+            comm["last_step"] = st
+        if not comm["count_matches_world"] and env.rank == 0:
+            print(f"[bench] WARNING: the communicator reports {comm['comm_count']} ranks but WORLD_SIZE is "
+                  f"{world}: collectives do not span the job", flush=True)
 
     if env.rank == 0:
         img_s = world * args.batch * args.steps / elapsed

@@ -1447,7 +1447,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("stream_ptr",
                              [](const pdt::RcclComm& c) { return reinterpret_cast<uintptr_t>(c.stream()); })
       .def("all_reduce", &pdt::RcclComm::all_reduce, py::arg("t"), py::arg("op") = "sum",
-           py::arg("wait_current") = true)
+           py::arg("wait_current") = true, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &pdt::RcclComm::broadcast, py::arg("t"), py::arg("root") = 0,
            py::arg("wait_current") = true)
       .def("reduce_scatter", &pdt::RcclComm::reduce_scatter, py::arg("inp"), py::arg("out"),
@@ -1458,7 +1458,11 @@ PYBIND11_MODULE(_C, m) {
       .def("current_wait_comm", &pdt::RcclComm::current_wait_comm)
       .def("synchronize", &pdt::RcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &pdt::RcclComm::barrier, py::call_guard<py::gil_scoped_release>())
-      .def("abort", &pdt::RcclComm::abort)
+      .def("abort", &pdt::RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("comm_count", &pdt::RcclComm::comm_count)
+      .def_static("version", &pdt::RcclComm::version)
+      .def_property_readonly("min_channels", [](const pdt::RcclComm& c) { return c.options().min_channels; })
+      .def_property_readonly("max_channels", [](const pdt::RcclComm& c) { return c.options().max_channels; })
       .def("check", &pdt::RcclComm::check)
       .def_property_readonly("healthy", &pdt::RcclComm::healthy)
       .def_property_readonly("error", &pdt::RcclComm::error)
@@ -1466,8 +1470,12 @@ PYBIND11_MODULE(_C, m) {
       .def("inject_delay", &pdt::RcclComm::inject_delay, py::arg("seconds"));
 
   py::class_<pdt::XgmiComm, std::shared_ptr<pdt::XgmiComm>>(m, "XgmiComm")
-      .def(py::init<int, int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"),
-           py::arg("device"), py::arg("numel"), py::arg("nbuckets"), py::arg("timeout") = 600.0)
+      .def(py::init<int, int, int, int64_t, int, double, std::string, int, bool>(), py::arg("rank"),
+           py::arg("world"), py::arg("device"), py::arg("numel"), py::arg("nbuckets"), py::arg("timeout") = 600.0,
+           py::arg("wire") = "fp32", py::arg("max_blocks") = 16, py::arg("exit_on_error") = false)
+      .def_property_readonly("wire", [](const pdt::XgmiComm& c) { return c.wire_bf16() ? "bf16" : "fp32"; })
+      .def_property_readonly("max_blocks", &pdt::XgmiComm::max_blocks)
+      .def_property_readonly("error_message", &pdt::XgmiComm::error_message)
       .def_property_readonly("rank", &pdt::XgmiComm::rank)
       .def_property_readonly("world", &pdt::XgmiComm::world)
       .def_property_readonly("device", &pdt::XgmiComm::device)

@@ -132,6 +132,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, cons
                rank, world, device, ncclGetErrorString(st));
     throw std::runtime_error(buf);
   }
+  gate_ = std::make_unique<AbortGate>([this]() { ncclCommAbort(comm_); });
   hip_check(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming), "hipEventCreate");
   barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device));
@@ -141,29 +142,35 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, cons
 RcclComm::~RcclComm() {
   stop_.store(true);
   if (monitor_.joinable()) monitor_.join();
-  if (comm_ && !aborted_.load() && !nonblocking_) {
-    // blocking communicator: destroy only once the comm stream has drained (bounded wait); a
-    // collective stuck on a dead peer is aborted instead of blocking our exit
-    const auto t0 = std::chrono::steady_clock::now();
-    hipError_t q;
-    while ((q = hipStreamQuery(stream())) == hipErrorNotReady && since(t0) < 10.0)
-      std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    if (q == hipSuccess) ncclCommDestroy(comm_);
-    else ncclCommAbort(comm_);
-  } else if (comm_ && !aborted_.load()) {
-    // non-blocking communicator: finalize (flushes outstanding work) must complete before
-    // destroy; a peer that died mid-teardown must not hang our exit, so the wait is bounded
-    ncclResult_t r = ncclCommFinalize(comm_);
-    ncclResult_t st = r;
-    const auto t0 = std::chrono::steady_clock::now();
-    while (r == ncclSuccess || r == ncclInProgress) {
-      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess || st != ncclInProgress) break;
-      if (since(t0) > 10.0) break;
-      std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    }
-    if (st == ncclSuccess) ncclCommDestroy(comm_);
-    else ncclCommAbort(comm_);
-  }  // aborted: ncclCommAbort already released the communicator
+  // teardown through the gate: waits for a call still inside the communicator, and does nothing
+  // if an abort already released it
+  if (gate_) {
+    gate_->finalize([&]() {
+      if (!nonblocking_) {
+        // blocking communicator: destroy only once the comm stream has drained (bounded wait); a
+        // collective stuck on a dead peer is aborted instead of blocking our exit
+        const auto t0 = std::chrono::steady_clock::now();
+        hipError_t q;
+        while ((q = hipStreamQuery(stream())) == hipErrorNotReady && since(t0) < 10.0)
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (q == hipSuccess) ncclCommDestroy(comm_);
+        else ncclCommAbort(comm_);
+      } else {
+        // non-blocking communicator: finalize (flushes outstanding work) must complete before
+        // destroy; a peer that died mid-teardown must not hang our exit, so the wait is bounded
+        ncclResult_t r = ncclCommFinalize(comm_);
+        ncclResult_t st = r;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (r == ncclSuccess || r == ncclInProgress) {
+          if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess || st != ncclInProgress) break;
+          if (since(t0) > 10.0) break;
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        if (st == ncclSuccess) ncclCommDestroy(comm_);
+        else ncclCommAbort(comm_);
+      }
+    });
+  }
   comm_ = nullptr;
   if (ev_a_) hipEventDestroy(ev_a_);
   if (ev_b_) hipEventDestroy(ev_b_);
@@ -171,13 +178,17 @@ RcclComm::~RcclComm() {
   for (hipEvent_t e : free_events_) hipEventDestroy(e);
 }
 
+// Both failure paths only REQUEST the abort: the gate runs ncclCommAbort at once when no thread
+// is inside an RCCL call on this communicator, else right after that call returns (the issuing
+// thread runs it on its way out; the monitor retries every poll).  failed_ is set first, so a
+// caller that has not yet entered the gate is refused by check() with the recorded error.
 void RcclComm::abort() {
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (error_.empty()) error_ = "RCCL communicator was aborted";
-    failed_.store(true);  // before the abort: no new call may reach the freed communicator
+    failed_.store(true);
   }
-  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+  if (gate_) gate_->request_abort();
 }
 
 void RcclComm::fail(const std::string& msg) {
@@ -190,7 +201,7 @@ void RcclComm::fail(const std::string& msg) {
   fprintf(stderr, "[rccl] rank %d: %s; aborting the communicator%s\n", rank_, msg.c_str(),
           opt_.exit_on_error ? " and exiting" : "");
   fflush(stderr);
-  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
+  if (gate_) gate_->request_abort();
   if (opt_.exit_on_error) std::_Exit(kCommExitCode);
 }
 
@@ -210,9 +221,14 @@ void RcclComm::monitor_loop() {
   const auto period = std::chrono::microseconds((int64_t)(opt_.poll_s * 1e6));
   while (!stop_.load()) {
     std::this_thread::sleep_for(period);
-    if (failed_.load()) continue;
-    ncclResult_t st = ncclSuccess;
-    if (ncclCommGetAsyncError(comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+    if (failed_.load()) {
+      gate_->drain();  // an abort still pending behind a call that was in flight
+      continue;
+    }
+    // skipped while another thread is inside an RCCL call (never blocks behind a slow enqueue)
+    ncclResult_t st = ncclSuccess, qr = ncclInternalError;
+    gate_->try_call([&]() { qr = ncclCommGetAsyncError(comm_, &st); });
+    if (qr == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
       fail(std::string("asynchronous RCCL error: ") + ncclGetErrorString(st));
       continue;
     }
@@ -270,26 +286,53 @@ void RcclComm::track(const char* what) {
   pending_.push_back({ev, std::chrono::steady_clock::now(), what});
 }
 
-void RcclComm::finish(ncclResult_t r, const char* what) {
-  if (r == ncclInProgress) {  // non-blocking communicator: the call completes asynchronously
-    const auto t0 = std::chrono::steady_clock::now();
-    ncclResult_t st = ncclInProgress;
-    while (st == ncclInProgress) {
-      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
-      if (st == ncclInProgress && since(t0) > opt_.init_timeout_s) break;
-      if (st == ncclInProgress) std::this_thread::yield();
-    }
-    r = st;
-    if (r == ncclInProgress) {
-      fail(std::string(what) + " still in progress after the init timeout");
-      check();
-    }
+ncclResult_t RcclComm::wait_async(const char* what) {
+  // non-blocking communicator: the call completes asynchronously (runs inside the gate)
+  (void)what;
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t st = ncclInProgress;
+  while (st == ncclInProgress) {
+    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+    if (st == ncclInProgress && since(t0) > opt_.init_timeout_s) break;
+    if (st == ncclInProgress) std::this_thread::yield();
+  }
+  return st;
+}
+
+template <class F>
+void RcclComm::issue(const char* what, F&& enqueue) {
+  check();
+  ncclResult_t r = ncclSuccess;
+  const bool ran = gate_->call([&]() {
+    r = enqueue();
+    if (r == ncclInProgress) r = wait_async(what);
+  });
+  if (!ran) {  // aborted between check() and the gate: refuse with the recorded error
+    check();
+    throw std::runtime_error(std::string("RCCL communicator (rank ") + std::to_string(rank_) +
+                             ") was aborted before " + what);
+  }
+  if (r == ncclInProgress) {
+    fail(std::string(what) + " still in progress after the init timeout");
+    check();
   }
   if (r != ncclSuccess) {
     fail(std::string(what) + " failed: " + ncclGetErrorString(r));
     check();
   }
   track(what);
+}
+
+int RcclComm::comm_count() {
+  int n = -1;
+  if (!gate_->call([&]() { rccl_check(ncclCommCount(comm_, &n), "ncclCommCount"); })) return -1;
+  return n;
+}
+
+int RcclComm::version() {
+  int v = 0;
+  rccl_check(ncclGetVersion(&v), "ncclGetVersion");
+  return v;
 }
 
 void RcclComm::inject_delay(double seconds) {
@@ -357,8 +400,7 @@ static void check_dev(const at::Tensor& t, int device) {
 }
 
 void RcclComm::all_reduce_raw(void* ptr, size_t count, ncclDataType_t dt, ncclRedOp_t op) {
-  check();
-  finish(ncclAllReduce(ptr, ptr, count, dt, op, comm_, stream()), "ncclAllReduce");
+  issue("ncclAllReduce", [&]() { return ncclAllReduce(ptr, ptr, count, dt, op, comm_, stream()); });
 }
 
 void RcclComm::all_reduce(const at::Tensor& t, const std::string& op, bool wait_current) {
@@ -371,8 +413,9 @@ void RcclComm::broadcast(const at::Tensor& t, int root, bool wait_current) {
   check_dev(t, device_);
   check();
   if (wait_current) comm_wait_current();
-  finish(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), root, comm_, stream()),
-         "ncclBroadcast");
+  issue("ncclBroadcast", [&]() {
+    return ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), root, comm_, stream());
+  });
 }
 
 void RcclComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, const std::string& op,
@@ -382,9 +425,10 @@ void RcclComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, const
   check();
   if (in.numel() != out.numel() * world_) throw std::runtime_error("reduce_scatter: size mismatch");
   if (wait_current) comm_wait_current();
-  finish(ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), dtype_of(in), op_of(op),
-                           comm_, stream()),
-         "ncclReduceScatter");
+  const ncclRedOp_t rop = op_of(op);
+  issue("ncclReduceScatter", [&]() {
+    return ncclReduceScatter(in.data_ptr(), out.data_ptr(), (size_t)out.numel(), dtype_of(in), rop, comm_, stream());
+  });
 }
 
 void RcclComm::all_gather(const at::Tensor& in, const at::Tensor& out, bool wait_current) {
@@ -393,8 +437,9 @@ void RcclComm::all_gather(const at::Tensor& in, const at::Tensor& out, bool wait
   check();
   if (out.numel() != in.numel() * world_) throw std::runtime_error("all_gather: size mismatch");
   if (wait_current) comm_wait_current();
-  finish(ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), dtype_of(in), comm_, stream()),
-         "ncclAllGather");
+  issue("ncclAllGather", [&]() {
+    return ncclAllGather(in.data_ptr(), out.data_ptr(), (size_t)in.numel(), dtype_of(in), comm_, stream());
+  });
 }
 
 void RcclComm::barrier() {

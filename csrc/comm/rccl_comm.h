@@ -16,6 +16,10 @@
 //    every later call on this communicator (and the reducer's next bucket launch) throws it --
 //    and, with `exit_on_error`, ends the process so the launcher's fail-fast tears the job down
 //    (ProcessGroupNCCL's async error handling);
+//  * every use of the communicator goes through an AbortGate (comm/abort_gate.h): an abort from
+//    the monitor or the user never frees it while another thread is inside an RCCL call on it --
+//    it runs as soon as that call returns -- and a call after the abort is refused with the
+//    recorded error instead of reaching the freed communicator;
 //  * per-communicator channel bounds (config.minCTAs / maxCTAs) are the RCCL knob for how many
 //    rings/channels a collective spreads over the 7 point-to-point xGMI links of a GPU.
 //
@@ -28,9 +32,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "comm/abort_gate.h"
+
 #include <atomic>
 #include <chrono>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -85,12 +92,21 @@ class RcclComm {
   // (a stalled peer without hanging the GPU)
   void inject_delay(double seconds);
   double init_seconds() const { return init_s_; }
+  // diagnostics: the rank count RCCL itself reports (ncclCommCount; -1 when aborted) and the
+  // RCCL library version (ncclGetVersion, e.g. 22606)
+  int comm_count();
+  static int version();
+  const RcclOptions& options() const { return opt_; }
 
   static ncclDataType_t dtype_of(const at::Tensor& t);
   static ncclRedOp_t op_of(const std::string& op);
 
  private:
-  void finish(ncclResult_t r, const char* what);  // ncclInProgress -> poll until done
+  // one gated RCCL call: `enqueue` runs under the abort gate (and, on a non-blocking
+  // communicator, the poll for its async enqueue); an error fails the communicator and throws
+  template <class F>
+  void issue(const char* what, F&& enqueue);
+  ncclResult_t wait_async(const char* what);      // ncclInProgress -> poll until done
   void track(const char* what);                   // completion event for the monitor
   void fail(const std::string& msg);
   void monitor_loop();
@@ -114,7 +130,7 @@ class RcclComm {
   std::vector<hipEvent_t> free_events_;
   std::string error_;
   std::atomic<bool> failed_{false};
-  std::atomic<bool> aborted_{false};
+  std::unique_ptr<AbortGate> gate_;  // created once the communicator exists
   std::atomic<bool> stop_{false};
   std::thread monitor_;
   double delay_s_ = 0.0;

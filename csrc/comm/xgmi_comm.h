@@ -9,15 +9,21 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace pdt {
 
 class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
  public:
-  XgmiComm(int rank, int world, int device, int64_t numel, int nbuckets, double timeout_s);
+  // wire: "fp32" or "bf16" (packed copies on the wire, fp32 sums); max_blocks: CU budget of the
+  // data kernels; exit_on_error: a host monitor thread ends the process (exit code 124, the
+  // watchdog's) as soon as the device error word is set -- a wait timed out or a peer failed
+  XgmiComm(int rank, int world, int device, int64_t numel, int nbuckets, double timeout_s,
+           const std::string& wire = "fp32", int max_blocks = 16, bool exit_on_error = false);
   ~XgmiComm();
 
   int rank() const { return rank_; }
@@ -26,7 +32,10 @@ class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
   int64_t numel() const { return numel_; }
   hipStream_t stream() const { return stream_.stream(); }
 
-  // IPC handles of (gradient buffer, reduced-shard buffer, flag array), concatenated
+  bool wire_bf16() const { return g16_ != nullptr; }
+  int max_blocks() const { return max_blocks_; }
+  // IPC handles of (gradient buffer, reduced-shard buffer, flag array[, bf16 gradient copy,
+  // bf16 reduced shards]), concatenated
   std::string ipc_handles() const;
   // map every peer's buffers from their handles (index = rank; the own entry is ignored)
   void open_peers(const std::vector<std::string>& handles);
@@ -47,8 +56,10 @@ class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
   void comm_wait_current();
   void current_wait_comm();
   void synchronize();
-  // 0 = healthy; otherwise 1 + 2*bucket (ready wait timed out) or 2 + 2*bucket (reduced wait)
+  // 0 = healthy; otherwise 1 + 2*bucket (ready wait timed out) or 2 + 2*bucket (reduced wait),
+  // with kXgmiPeerFailed | (peer << 16) set when the wait saw that peer's POISON signal
   int error_code() const;
+  std::string error_message() const;  // "" when healthy
   void check() const;
 
  private:
@@ -60,11 +71,20 @@ class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
   float* g_ = nullptr;
   float* red_ = nullptr;
   unsigned* flags_ = nullptr;
+  uint16_t* g16_ = nullptr;   // bf16 wire only
+  uint16_t* red16_ = nullptr;
+  int max_blocks_ = 16;
+  bool exit_on_error_ = false;
+  std::atomic<bool> stop_{false};
+  std::thread monitor_;
+  void monitor_loop();
   unsigned* err_host_ = nullptr;  // pinned, device-visible error word
   unsigned* err_dev_ = nullptr;
   const float* gp_[8] = {};
   const float* rp_[8] = {};
   unsigned* fp_[8] = {};
+  const uint16_t* g16p_[8] = {};
+  const uint16_t* r16p_[8] = {};
   std::vector<void*> opened_;
   std::vector<unsigned> epoch_;
   bool linked_ = false;

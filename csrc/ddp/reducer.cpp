@@ -33,7 +33,7 @@ struct ReducerState {
 
   std::vector<std::shared_ptr<torch::autograd::Node>> accumulators;
 
-  // comm timing (RCCL path only): first bucket start / last bucket end on the comm stream, and
+  // comm timing (RCCL and xGMI paths): first bucket start / last bucket end on the comm stream, and
   // the end of backward compute on the caller's stream -> all-reduce time and its exposed tail
   bool timing = false;
   bool timed = false;  // events of the last finished iteration are valid
@@ -81,6 +81,7 @@ struct ReducerState {
         hipEventRecord(ev_aux, aux);
         hipStreamWaitEvent(xgmi->stream(), ev_aux, 0);
       }
+      if (timing && first) hipEventRecord(ev_start, xgmi->stream());
       xgmi->reduce_bucket((int)b, flat_off[b], flats[b].numel(), average);
       return;
     }
@@ -181,6 +182,13 @@ struct ReducerState {
     for (size_t i = 0; i < params.size(); ++i)
       if (!param_ready[i]) mark_param((int64_t)i, /*zero_if_missing=*/true);
     if (xgmi) {
+      if (timing) {
+        c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
+        hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)xgmi->device()).stream();
+        hipEventRecord(ev_bwd, cur);
+        hipEventRecord(ev_end, xgmi->stream());
+        timed = !launch_order.empty();
+      }
       xgmi->current_wait_comm();
     } else if (comm) {
       if (timing) {
@@ -272,9 +280,9 @@ Reducer::~Reducer() {
 
 void Reducer::set_timing(bool on) {
   std::lock_guard<std::mutex> lk(st_->mu);
-  if (on && !st_->comm) throw std::runtime_error("Reducer timing needs the RCCL communicator");
+  if (on && !st_->comm && !st_->xgmi) throw std::runtime_error("Reducer timing needs a native communicator");
   if (on && !st_->ev_start) {
-    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->comm->device());
+    c10::hip::HIPGuard guard((c10::DeviceIndex)(st_->comm ? st_->comm->device() : st_->xgmi->device()));
     for (hipEvent_t* e : {&st_->ev_start, &st_->ev_end, &st_->ev_bwd})
       if (hipEventCreate(e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
   }

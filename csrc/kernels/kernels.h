@@ -270,14 +270,24 @@ void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uin
 
 // ---------------------------------------------------------------- xgmi.hip
 // Direct one-hop all-reduce of elements [lo, lo + count) of every rank's fp32 gradient buffer
-// (bucket `bucket`, epoch `epoch`): signal ready -> wait (bounded) -> reduce own shard from all
-// peers -> signal reduced -> wait -> gather every shard back (divided by world when `average`).
-// g / red / flags: device pointers of every rank's buffers as mapped in this process; err: device
-// view of a host word set to a nonzero code when a wait passes timeout_ticks (wall clock).
+// (bucket `bucket`, epoch `epoch`): (bf16 wire: pack) signal ready -> wait (bounded) -> reduce own
+// shard from all peers -> signal reduced -> wait -> gather every shard back (divided by world when
+// `average`).  Buffers: device pointers of every rank's buffers as mapped in this process (g16 /
+// red16 null: fp32 wire); err: device view of a host word set to a nonzero code when a wait passes
+// timeout_ticks (wall clock) or a peer signalled POISON (failed).  The data kernels use at most
+// `max_blocks` workgroups (the CU budget beside the backward pass).
+constexpr unsigned kXgmiPeerFailed = 0x80000000u;  // err | (peer << 16) | code: a peer failed first
+struct XgmiBuffers {
+  const float* g[8];
+  const float* red[8];
+  unsigned* flags[8];
+  const uint16_t* g16[8];
+  const uint16_t* red16[8];
+};
 int xgmi_max_ranks();
-void launch_xgmi_bucket(const float* const* g, const float* const* red, unsigned* const* flags, int world,
-                        int rank, int bucket, int64_t lo, int64_t count, unsigned epoch, bool average,
-                        uint64_t timeout_ticks, unsigned* err, hipStream_t st, int phase_lo = 0,
-                        int phase_hi = 5);
+int64_t xgmi_shard(int64_t lo, int64_t count, int world);
+void launch_xgmi_bucket(const XgmiBuffers& bufs, int world, int rank, int bucket, int64_t lo, int64_t count,
+                        unsigned epoch, bool average, uint64_t timeout_ticks, unsigned* err, hipStream_t st,
+                        int phase_lo = 0, int phase_hi = 5, int max_blocks = 16);
 
 }  // namespace pdt

@@ -93,12 +93,14 @@ class CommOptions:
     monitor aborts the communicator (default: on when world > 1).  ``min_channels`` /
     ``max_channels`` bound the RCCL channels (rings) a collective spreads over (``ncclConfig_t``
     minCTAs / maxCTAs; 0 = RCCL's choice); the env knob ``PDT_RCCL_CHANNELS=min[,max]`` sets them
-    too."""
+    too.  ``xgmi_blocks`` is the same budget for the direct xGMI backend: its reduce-scatter /
+    all-gather kernels use at most that many workgroups beside the backward pass."""
     init_timeout: float = DEFAULT_TIMEOUT_S
     op_timeout: float = DEFAULT_TIMEOUT_S
     exit_on_error: Optional[bool] = None
     min_channels: int = 0
     max_channels: int = 0
+    xgmi_blocks: int = 16  # CU budget of the xGMI backend's data kernels (PDT_XGMI_BLOCKS)
 
     @classmethod
     def from_env(cls, timeout: Optional[float] = None, **kw) -> "CommOptions":
@@ -108,6 +110,8 @@ class CommOptions:
             o.init_timeout = o.op_timeout = float(t)
         if os.environ.get("PDT_COMM_TIMEOUT"):
             o.init_timeout = o.op_timeout = float(os.environ["PDT_COMM_TIMEOUT"])
+        if os.environ.get("PDT_XGMI_BLOCKS"):
+            o.xgmi_blocks = max(1, int(os.environ["PDT_XGMI_BLOCKS"]))
         ch = os.environ.get("PDT_RCCL_CHANNELS")
         if ch and not (o.min_channels or o.max_channels):
             parts = [int(x) for x in ch.split(",")]

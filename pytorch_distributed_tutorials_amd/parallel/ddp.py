@@ -196,12 +196,13 @@ class DistributedDataParallel(nn.Module):
         if comm == "xgmi":
             if self.device.type != "cuda" or not native_available():
                 raise RuntimeError("comm='xgmi' needs a GPU device and the native extension")
-            if wire_dtype != "fp32":
-                raise ValueError("comm='xgmi' reduces fp32 gradients (wire_dtype='fp32')")
             from .xgmi import xgmi_comm
             self._collective = True
+            # wire_dtype="bf16": peers read packed bf16 copies (half the link bytes), sums in fp32
             self.xgmi = xgmi_comm(self.device, sum(p.numel() for p in params), len(plan), process_group,
-                                  timeout=self.comm_options.init_timeout)
+                                  timeout=self.comm_options.init_timeout, wire=wire_dtype,
+                                  max_blocks=self.comm_options.xgmi_blocks,
+                                  exit_on_error=self.comm_options.exit_on_error)
             grad_storage = self.xgmi.grad_buffer()
         self.space = FlatParamSpace([params[i] for i in layout], grad_flat=grad_storage)
         self.bucket_ranges = []
@@ -362,8 +363,9 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------- metrics
     def enable_comm_timing(self, on: bool = True) -> bool:
-        """Record HIP events around each iteration's all-reduces (native RCCL path only)."""
-        if self.reducer is None or self.comm is None or not hasattr(self.reducer, "set_timing"):
+        """Record HIP events around each iteration's all-reduces (native RCCL / xGMI paths)."""
+        if self.reducer is None or (self.comm is None and self.xgmi is None) \
+                or not hasattr(self.reducer, "set_timing"):
             return False
         self.reducer.set_timing(on)
         self._timing = on
@@ -378,10 +380,36 @@ class DistributedDataParallel(nn.Module):
             return None
         return {"comm_ms": total, "exposed_ms": exposed}
 
+    def check_comm(self) -> None:
+        """Raise the recorded error if a native communicator failed (RCCL monitor abort / timeout,
+        or an xGMI wait that timed out or saw a failed peer)."""
+        if self.comm is not None:
+            self.comm.check()
+        if self.xgmi is not None:
+            self.xgmi.check()
+
     def abort(self) -> None:
         """Abort the native communicator (unblocks kernels waiting on a dead peer)."""
         if self.comm is not None:
             self.comm.abort()
+
+    def comm_diagnostics(self) -> dict:
+        """What the communicator itself reports (for the scaling run's JSON): backend, the rank
+        count RCCL sees (``ncclCommCount``) against ``WORLD_SIZE``, RCCL version, channel bounds /
+        xGMI CU budget, wire format and bucket sizes."""
+        d = {"world_size": self.world_size, "wire_dtype": self.wire_dtype,
+             "buckets_mb": [round(b / 2**20, 3) for b in self.bucket_bytes]}
+        if self.xgmi is not None:
+            d.update(backend="xgmi", comm_count=self.xgmi.world, xgmi_blocks=self.xgmi.max_blocks,
+                     xgmi_wire=self.xgmi.wire, healthy=self.xgmi.error_code == 0)
+        elif self.comm is not None:
+            d.update(backend="rccl", comm_count=self.comm.comm_count(), rccl_version=self.comm.version(),
+                     channels=[self.comm.min_channels, self.comm.max_channels], healthy=self.comm.healthy)
+        else:
+            d.update(backend=("python-" + pcomm.backend_name()) if self._collective else "none",
+                     comm_count=self.world_size)
+        d["count_matches_world"] = d["comm_count"] == self.world_size
+        return d
 
     def bucket_info(self) -> dict:
         return {"num_buckets": len(self.bucket_ranges), "bucket_elems": list(self.bucket_sizes),

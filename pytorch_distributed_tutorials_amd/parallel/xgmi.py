@@ -26,20 +26,29 @@ _TAG = itertools.count()
 
 
 def xgmi_comm(device: torch.device, numel: int, nbuckets: int, pg=None,
-              timeout: float = DEFAULT_TIMEOUT_S):
-    """Create this rank's ``XgmiComm`` and map every peer's buffers (collective over ``pg``)."""
+              timeout: float = DEFAULT_TIMEOUT_S, wire: str = "fp32", max_blocks: int = 16,
+              exit_on_error=None):
+    """Create this rank's ``XgmiComm`` and map every peer's buffers (collective over ``pg``).
+
+    ``wire``: "fp32" or "bf16" (half the xGMI bytes; fp32 sums); ``max_blocks``: CU budget of
+    the data kernels; ``exit_on_error`` (default: world > 1): the host monitor ends the process
+    when a bounded wait fails or a peer signals that it failed."""
     from ..ops._ext import native
     C = native()
     if not (dist.is_available() and dist.is_initialized()):
-        comm = C.XgmiComm(0, 1, device.index, numel, nbuckets, timeout)
+        comm = C.XgmiComm(0, 1, device.index, numel, nbuckets, timeout, wire, max_blocks,
+                          bool(exit_on_error))
         comm.link_local([comm])
         return comm
     rank, world = dist.get_rank(pg), dist.get_world_size(pg)
+    if exit_on_error is None:
+        exit_on_error = world > 1
     store = dist.distributed_c10d._get_default_store()
     tag = f"pdt/xgmi/{next(_TAG)}"
     comm, err = None, ""
     try:
-        comm = C.XgmiComm(rank, world, device.index, numel, nbuckets, timeout)
+        comm = C.XgmiComm(rank, world, device.index, numel, nbuckets, timeout, wire, max_blocks,
+                          bool(exit_on_error))
         store.set(f"{tag}/h/{rank}", b"1" + comm.ipc_handles())
     except Exception as e:  # noqa: BLE001 -- reported to every rank
         err = f"{type(e).__name__}: {e}"
@@ -69,12 +78,14 @@ def xgmi_comm(device: torch.device, numel: int, nbuckets: int, pg=None,
     return comm
 
 
-def local_group(device: torch.device, numel: int, nbuckets: int, world: int, timeout: float = 10.0):
+def local_group(device: torch.device, numel: int, nbuckets: int, world: int, timeout: float = 10.0,
+                wire: str = "fp32", max_blocks: int = 16):
     """``world`` in-process ranks linked by raw pointers (no IPC): tests of the kernels and the
     protocol on one GPU without separate processes."""
     from ..ops._ext import native
     C = native()
-    comms = [C.XgmiComm(q, world, device.index, numel, nbuckets, timeout) for q in range(world)]
+    comms = [C.XgmiComm(q, world, device.index, numel, nbuckets, timeout, wire, max_blocks, False)
+             for q in range(world)]
     for c in comms:
         c.link_local(comms)
     return comms

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import os
+import sys
 from typing import Optional
 
 import torch
@@ -274,6 +275,11 @@ def main(argv: Optional[list] = None) -> int:
                 # evaluates the wrapped module itself: no collective, same buffers
                 accuracy = evaluate(model=ddp_model.module if graph_step is not None else ddp_model,
                                     device=device, test_loader=test_loader)
+            # never persist weights a failed all-reduce left on this rank (a timed-out xGMI wait
+            # NaN-poisons its bucket; a failed RCCL communicator is marked unusable): raise first
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            ddp_model.check_comm()
             save_checkpoint(ddp_model, model_filepath, optimizer, epoch)
             print("-" * 75)
             print("Epoch: {}, Accuracy: {}".format(epoch, accuracy))
@@ -319,6 +325,17 @@ def main(argv: Optional[list] = None) -> int:
             break
     if watchdog is not None:
         watchdog.stop()
+    if env.world_size > 1:
+        # every rank is past its last collective: end the process here (as bench.py does) rather
+        # than in interpreter teardown, where the reducer's native communicators (RCCL, and the
+        # xGMI buffers peers may still map) would be destroyed in an unspecified order with torch's
+        torch.distributed.barrier()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        destroy()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     destroy()
     return 0
 

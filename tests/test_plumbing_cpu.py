@@ -247,6 +247,32 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert abs(d["value"] - 8 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
 
 
+def test_bench_two_ranks_native_reports_comm_diagnostics(tmp_path):
+    """the scaling run's JSON must be diagnosable -- the rank count the
+    communicator itself reports (vs WORLD_SIZE), backend, wire format and bucket sizes ride in
+    config.comm (native impl, 2 gloo ranks on the CPU; the RCCL twin is
+    tests/test_rccl_gpu.py::test_bench_force_comm_reports_diagnostics)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_PORT=str(free_port()), OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--arch", "resnet18",
+                        "--image-size", "32", "--num-classes", "10", "--batch", "4", "--steps", "2",
+                        "--warmup", "1", "--impl", "native", "--backend", "gloo"],
+                       cwd=root, env=env, timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    c = json.loads(lines[0])["config"]["comm"]
+    assert c["world_size"] == 2 and c["comm_count"] == 2 and c["count_matches_world"]
+    assert c["backend"] == "python-gloo" and c["wire_dtype"] == "fp32"
+    assert len(c["buckets_mb"]) >= 2 and all(b > 0 for b in c["buckets_mb"])
+    assert "WARNING" not in r.stdout
+
+
 def test_bn_counter_list_cache_follows_mode_and_surgery():
     """bump_bn_counters caches the model's BatchNorm list (host issue); the cached counters follow
     train()/eval() and a replaced counter buffer, and forget_bn_modules picks up new modules."""

@@ -283,3 +283,59 @@ def test_bench_force_comm_json(gpu, tmp_path):
     assert cfg["comm"]["buckets_mb"][-1] <= 2.0
     assert cfg["comm"]["last_step"] is not None
     assert res["value"] > 0 and math.isfinite(cfg["final_loss"])
+
+
+def test_rccl_abort_spam_while_issuing(gpu):
+    # abort() from other threads while a thread issues collectives on the same
+    # world-1 communicator.  Every use goes through the abort gate: the issuing thread must end
+    # with the recorded error (never a crash / use-after-free), repeatedly, and the process must
+    # exit cleanly.  all_reduce and abort release the GIL, so the threads really overlap.
+    code = (
+        "import threading, time, torch\n"
+        "from pytorch_distributed_tutorials_amd.ops import _ext\n"
+        "C = _ext.native()\n"
+        "x = torch.ones(4096, device='cuda')\n"
+        "ok = 0\n"
+        "for rnd in range(6):\n"
+        "    c = C.RcclComm(C.RcclComm.unique_id(), 0, 1, 0, init_timeout=60.0, op_timeout=30.0)\n"
+        "    assert c.comm_count() == 1\n"
+        "    res = {}\n"
+        "    def issue():\n"
+        "        n = 0\n"
+        "        try:\n"
+        "            while True:\n"
+        "                c.all_reduce(x, 'sum'); n += 1\n"
+        "        except RuntimeError as e:\n"
+        "            res['err'] = str(e); res['n'] = n\n"
+        "    t = threading.Thread(target=issue); t.start()\n"
+        "    time.sleep(0.05 + 0.02 * rnd)\n"
+        "    spam = [threading.Thread(target=lambda: [c.abort() for _ in range(200)]) for _ in range(3)]\n"
+        "    [s.start() for s in spam]; [s.join() for s in spam]\n"
+        "    t.join(timeout=30)\n"
+        "    assert not t.is_alive(), 'issuing thread hung'\n"
+        "    assert 'abort' in res.get('err', ''), res\n"
+        "    assert not c.healthy and c.comm_count() == -1\n"
+        "    del c\n"
+        "    ok += 1\n"
+        "torch.cuda.synchronize()\n"
+        "print('ABORT_SPAM_OK', ok, C.RcclComm.version())\n")
+    r = _py(code, timeout=150)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "ABORT_SPAM_OK 6" in r.stdout, r.stdout
+
+
+def test_bench_force_comm_reports_diagnostics(gpu, tmp_path):
+    # bench.py's JSON carries what RCCL itself reports (ncclCommCount, version,
+    # channel bounds) and one untimed step's all-reduce time / exposed tail from the reducer's
+    # events, so the driver's first 8-GPU run is diagnosable
+    import json
+    out = tmp_path / "b.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--arch", "resnet18", "--image-size", "64",
+                        "--batch", "32", "--steps", "2", "--warmup", "1", "--force-comm", "--json-out", str(out)],
+                       cwd=ROOT, timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    c = json.loads(out.read_text())["config"]["comm"]
+    assert c["backend"] == "rccl" and c["native_comm"] and c["comm_count"] == 1 and c["count_matches_world"]
+    assert c["rccl_version"] >= 20000 and c["healthy"]
+    assert c["comm_ms"] >= 0 and 0 <= c["exposed_ms"] <= c["comm_ms"] + 1e-3
+    assert len(c["channels"]) == 2

@@ -81,6 +81,86 @@ def test_xgmi_absent_peer_times_out_without_hanging(gpu):
         comms[0].reduce_bucket(0, 0, 8192, True)
 
 
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_xgmi_unaligned_buckets_and_cu_budget(gpu, wire):
+    # buckets at odd offsets / lengths (param boundaries are not 8-aligned in general): the vector
+    # body + scalar edges cover every element exactly once, with the grid capped at 2 and 64
+    # workgroups; fp32 wire bitwise, bf16 wire within two bf16 roundings
+    from pytorch_distributed_tutorials_amd.parallel.xgmi import local_group, reduce_local_group
+    n = 100_003
+    buckets = [(0, 5), (5, 33_331), (33_336, 1), (33_337, 66_661)]
+    for blocks in (2, 64):
+        comms = local_group(gpu, n, len(buckets), 3, timeout=20.0, wire=wire, max_blocks=blocks)
+        assert comms[0].max_blocks == blocks and comms[0].wire == wire
+        g = torch.Generator().manual_seed(blocks)
+        data = [torch.randn(n, generator=g) for _ in range(3)]
+        for c, d in zip(comms, data):
+            c.grad_buffer().copy_(d.to(gpu))
+        torch.cuda.synchronize()
+        for bi, (off, cnt) in enumerate(buckets):
+            reduce_local_group(comms, bi, off, cnt, True)
+        for c in comms:
+            c.synchronize()
+        ref = (data[0] + data[1] + data[2]) / 3
+        end = buckets[-1][0] + buckets[-1][1]
+        for q, c in enumerate(comms):
+            got = c.grad_buffer().cpu()
+            if wire == "fp32":
+                assert torch.equal(got[:end], ref[:end]), (blocks, q)
+            else:
+                err = (got[:end] - ref[:end]).abs()
+                assert float(err.max()) < 3 * 2 ** -8 * float(ref[:end].abs().max() + 1), (blocks, q)
+            assert torch.equal(got[end:], data[q][end:])
+        del comms
+
+
+def test_xgmi_bf16_wire_error_at_8_ranks(gpu):
+    # the bound tests/test_wire_cpu.py pins for RCCL's bf16 wire at 8 ranks: relative L2 < 1 % and
+    # within 4x of rounding the exact average to bf16 once.  Here: one rounding of every input and
+    # one of the fp32-summed shard, so the error is close to 2x the single rounding.
+    from pytorch_distributed_tutorials_amd.parallel.xgmi import local_group, reduce_local_group
+    n = 262_144 + 17
+    comms = local_group(gpu, n, 1, 8, timeout=20.0, wire="bf16")
+    g = torch.Generator().manual_seed(7)
+    data = [torch.randn(n, generator=g, dtype=torch.float64) * (q + 1) for q in range(8)]
+    for c, d in zip(comms, data):
+        c.grad_buffer().copy_(d.float().to(gpu))
+    torch.cuda.synchronize()
+    reduce_local_group(comms, 0, 0, n, True)
+    for c in comms:
+        c.synchronize()
+    exact = sum(d.float().double() for d in data) / 8
+    def rel(t):
+        return float((t.double() - exact).norm() / exact.norm())
+    once = rel(exact.to(torch.bfloat16))
+    got = [c.grad_buffer().cpu() for c in comms]
+    for t in got:
+        assert torch.equal(t, got[0])  # every rank holds the same reduced gradient
+    r = rel(got[0])
+    assert r < 1e-2 and r < 4 * once and r > 1e-5, (r, once)
+
+
+def test_xgmi_failure_poisons_late_peer(gpu):
+    # rank 0's ready-wait times out (rank 1 arrives late).  Rank 0 must signal
+    # POISON -- not a current epoch -- so the late rank 1 fails too instead of gathering rank 0's
+    # never-reduced shard; both ranks' buckets are NaN-poisoned (no silent step on local gradients)
+    from pytorch_distributed_tutorials_amd.parallel.xgmi import local_group
+    n = 8192
+    comms = local_group(gpu, n, 1, 2, timeout=0.5)
+    for q, c in enumerate(comms):
+        c.grad_buffer().fill_(float(q + 1))
+    torch.cuda.synchronize()
+    comms[0].reduce_bucket(0, 0, n, True)      # rank 1 has not signalled: times out after 0.5 s
+    with pytest.raises(RuntimeError, match="never marked their gradients ready"):
+        comms[0].synchronize()
+    comms[1].reduce_bucket(0, 0, n, True)      # the late peer: sees rank 0's POISON
+    with pytest.raises(RuntimeError, match="peer rank 0 failed first"):
+        comms[1].synchronize()
+    assert comms[1].error_code & 0x80000000
+    for c in comms:
+        assert torch.isnan(c.grad_buffer()).all()
+
+
 def _launch(mode, nproc):
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
