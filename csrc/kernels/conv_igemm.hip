@@ -1104,6 +1104,206 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
 
 
 // ============================================================================
+//          NT 256x256, quadrant-phased pipeline (long-K fwd / dgrad, bf16)
+// ============================================================================
+// The 2-stage NT main loop above issues step k+1 at the top of step k and drains every DMA
+// (vmcnt 0) at its bottom: a load has exactly one K-step of MFMA time to land, and on the
+// 1-block-per-CU 256x256 tile that step is ~1 us -- about one L2->LDS DMA latency under load, so
+// long-K GEMMs stall once per step (4096^3: 642 TF/s vs hipBLASLt 1,524).
+//
+// This kernel splits each 64-deep K-step of the 256x256 tile into FOUR phases, one per output
+// quadrant (X half hx, W half hw), so a quarter tile (one half of one operand, 16 KB) is dead as
+// soon as its last phase has read it, and is refilled right then with the same quarter of step
+// s+2 (two LDS stages, 128 KB):
+//     P0: Q(0,0)  reads X0, W0 (fragments kept in registers)  -> both dead
+//     P1: Q(0,1)  reads W1 (kept), reuses X0                    -> issue X0(s+2), W0(s+2)
+//     P2: Q(1,0)  reads X1 (kept), reuses W0                    -> issue W1(s+2)
+//     P3: Q(1,1)  reuses X1, W1 (no LDS reads)                  -> issue X1(s+2)
+// Every quarter is issued 7 phases (1.75 K-steps) before its first read, in the order the next
+// steps consume them, and each phase waits with a COUNTED vmcnt for exactly the quarters it
+// reads (12 / 10 / 12 glds younger than them), never vmcnt(0): loads stay in flight across the
+// barriers.  One barrier per phase covers both hazards: RAW (every wave's DMA pieces of the
+// quarters read in this phase have landed: each wave's counted wait precedes it) and WAR (every
+// wave finished reading the quarter refilled in this phase: reads are consumed, lgkmcnt 0, by the
+// previous phase's MFMAs).  Steps past the end issue all-OOB pieces (zero fill, no memory
+// traffic) so the counts stay static.
+// Rows are permuted so that each wave's 4 quadrant sub-tiles form ONE contiguous 128x64 output
+// tile (8 waves = 2 (M) x 4 (N)): X half hx holds GEMM rows {wm*128 + hx*64 + [0,64)}, W half
+// hw holds channels {wn*64 + hw*32 + [0,32)}, so nt_epilogue runs unchanged (WM 2, WN 4,
+// TM 8, TN 4).  C64 (per-tap 64-channel K-steps) loader only.
+// barrier that also retires this wave's own LDS reads first: the quarter refilled right after it
+// must not have a fragment read of any wave still in flight (the MFMAs that consume the reads
+// are not memory operations, so the compiler may place them -- and their lgkmcnt wait -- after
+// an asm barrier)
+__device__ __forceinline__ void lds_barrier_rd() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
+  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
+  static_assert(CFG::BM == 256 && CFG::BN == 256 && CFG::NT == 512, "ntq geometry");
+  constexpr int EB = 2, KE = 64, QB = 16384;  // quarter: 128 rows x 128 B
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntn = (P.Nout + 255) / 256;
+  const int ntm = (P.M + 255) / 256;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
+  const int m0 = tmi * 256, n0 = tni * 256;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane >> 3, lj = lane & 7;  // row within a DMA instruction (8 rows), LDS chunk slot
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
+
+  // this lane's DMA rows: piece i (0, 1) of half h covers half-local rows r = (wid*2 + i)*8 + lr
+  int a_base[2][2], b_row[2][2], b_c[2][2];
+  uint32_t a_inv[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wid * 2 + i) * 8 + lr;
+      const int sc = lj ^ ((r >> 1) & 7);  // source chunk landing in slot lj (read side: swz128)
+      b_c[h][i] = sc;
+      const int m = m0 + (r >> 6) * 128 + h * 64 + (r & 63);
+      int pix = 0, h0 = -(1 << 20), w0 = 0;
+      if (m < P.M) {
+        const uint32_t n = fdiv((uint32_t)m, P.div_ij);
+        const uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+        const uint32_t ii = fdiv(rem, P.div_j);
+        const uint32_t jj = rem - ii * (uint32_t)P.Mj;
+        pix = (int)n * P.HA * P.WA;
+        h0 = (int)ii * P.ash + P.aoff_h;
+        w0 = (int)jj * P.asw + P.aoff_w;
+      }
+      a_base[h][i] = (pix + h0 * P.WA + w0) * P.CA * EB + sc * 16;
+      // tap validity bitmask (see igemm_nt_kernel): bit t set = tap t reads outside the image
+      const int nr = P.tnr, ns = P.tns;
+      const int hb = h0 + P.dr0, wb = w0 + P.ds0;
+      const int hlo = P.dstep > 0 ? max(0, -hb) : max(0, hb - P.HA + 1);
+      const int hhi = P.dstep > 0 ? min(nr, P.HA - hb) : min(nr, hb + 1);
+      const int wlo = P.dstep > 0 ? max(0, -wb) : max(0, wb - P.WA + 1);
+      const int whi = P.dstep > 0 ? min(ns, P.WA - wb) : min(ns, wb + 1);
+      const uint32_t hm = hhi > hlo ? (1u << (hhi & 31)) - (1u << (hlo & 31)) : 0u;
+      const uint32_t wmk = whi > wlo ? (1u << (whi & 31)) - (1u << (wlo & 31)) : 0u;
+      uint32_t spread = 0u;
+      for (int ti = 0; ti < nr; ++ti) spread |= ((hm >> ti) & 1u) << (ti * ns);
+      a_inv[h][i] = ~(wmk * spread);
+      const int ch = n0 + (r >> 5) * 64 + h * 32 + (r & 31);
+      b_row[h][i] = ch < P.Nout ? ch * P.Kg : -1;
+    }
+
+  // K-step state of the NEXT step to issue (ti, tj, channel block), advanced once per step
+  const int nk = P.ntaps * (P.CA / KE);
+  int q_ti = 0, q_tj = 0, q_chb = 0, q_kt = 0;
+  auto advance = [&]() {
+    ++q_kt;
+    q_chb += KE;
+    if (q_chb == P.CA) {
+      q_chb = 0;
+      if (++q_tj == P.tns) { q_tj = 0; ++q_ti; }
+    }
+  };
+  // quarter (operand X = 0 / W = 1, half h) of the step held by the tracker, into stage `st`
+  auto issue = [&](int op, int h, int st) {
+    const bool valid = q_kt < nk;
+    char* dst = smem + st * 65536 + (op * 2 + h) * QB + wid * 2048;
+    if (op == 0) {
+      const int tap = q_ti * P.tns + q_tj;
+      const int dr = P.dr0 + q_ti * P.dstep, ds = P.ds0 + q_tj * P.dstep;
+      const int tdelta = ((dr * P.WA + ds) * P.CA + q_chb) * EB;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[h][i], (unsigned)tap, 1u) |
+                                (valid ? 0u : 0xffffffffu);
+        glds16(ra, dst + i * 1024, (uint32_t)(a_base[h][i] + tdelta) | poison);
+      }
+    } else {
+      const int tbo = ((P.tr0 + q_ti * P.tstep) * P.S + (P.ts0 + q_tj * P.tstep)) * P.CA + q_chb;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t off = (valid && b_row[h][i] >= 0) ? (uint32_t)((b_row[h][i] + tbo) * EB + b_c[h][i] * 16) : OOB;
+        glds16(rb, dst + i * 1024, off);
+      }
+    }
+  };
+
+  const int wm = wid % 2, wn = wid / 2;
+  const int fr = lane & 15, fq = lane >> 4;
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: steps 0 and 1, every quarter in consumption order (X0, W0, W1, X1)
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    issue(0, 0, st); issue(1, 0, st); issue(1, 1, st); issue(0, 1, st);
+    advance();
+  }
+  // fragments: X rows of this wave in a half = wm*64 + i*16 + fr (4 tiles); W rows = wn*32 + j*16 + fr
+  auto read_x = [&](const char* base, v4i (&f)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        f[i][ks] = *reinterpret_cast<const v4i*>(base + swz128(wm * 64 + i * 16 + fr, ks * 4 + fq));
+  };
+  auto read_w = [&](const char* base, v4i (&f)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        f[j][ks] = *reinterpret_cast<const v4i*>(base + swz128(wn * 32 + j * 16 + fr, ks * 4 + fq));
+  };
+  auto mma = [&](int i0, int j0, const v4i (&xf)[4][2], const v4i (&wf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i0 + i][j0 + j] = mfma16(wf[j][ks], xf[i][ks], acc[i0 + i][j0 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  v4i x0[4][2], x1[4][2], w0f[2][2], w1f[2][2];
+  for (int s = 0; s < nk; ++s) {
+    const int st = s & 1;
+    const char* base = smem + st * 65536;
+    // P0: Q(0,0)
+    wait_vm<12>();
+    lds_barrier_rd();
+    read_x(base, x0);
+    read_w(base + 2 * QB, w0f);
+    mma(0, 0, x0, w0f);
+    // P1: Q(0,1); X0 and W0 of this stage are dead -> refill with step s+2
+    wait_vm<10>();
+    lds_barrier_rd();
+    issue(0, 0, st);
+    issue(1, 0, st);
+    read_w(base + 3 * QB, w1f);
+    mma(0, 2, x0, w1f);
+    // P2: Q(1,0); W1 dead
+    wait_vm<12>();
+    lds_barrier_rd();
+    issue(1, 1, st);
+    read_x(base + QB, x1);
+    mma(4, 0, x1, w0f);
+    // P3: Q(1,1) from registers; X1 dead
+    lds_barrier_rd();
+    issue(0, 1, st);
+    advance();
+    mma(4, 2, x1, w1f);
+  }
+  wait_vm<0>();
+  lds_barrier();  // every DMA landed and every fragment read done before the epilogue reuses LDS
+  nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, m0, n0, tmi);
+}
+
+// ============================================================================
 //                      TN implicit GEMM (wgrad, split-K)
 // ============================================================================
 struct TnArgs {
@@ -1167,10 +1367,16 @@ __device__ __forceinline__ int swz_img(int row, int chunk) {
   else return swz128_tr(row, chunk);
 }
 
-template <int BMG, int BNG, int STAGES>
+// RING: the stages are K32 slots (32 reduction rows of both operands) in a ring of STAGES = 4,
+// refilled three slots (1.5 K64 steps) ahead with counted vmcnt waits and one barrier per slot,
+// instead of two K64 stages with one step of lead and a vmcnt(0) drain per step -- the same LDS
+// (64 KB at BMG 128: two blocks per CU), twice the load lead.  Fragment reads are unchanged: a
+// slot is exactly one 32-row k-sub-step of the K64 image (the row swizzles repeat every 16 rows).
+template <int BMG, int BNG, int STAGES, bool RING = false>
 struct TnCfg {
   static_assert(BNG == 128 && (BMG == 64 || BMG == 128 || BMG == 256), "TN tile shapes");
-  static_assert(STAGES >= 2 && STAGES <= 3, "pipeline depth");
+  static_assert(RING ? STAGES == 4 : (STAGES >= 2 && STAGES <= 3), "pipeline depth");
+  static constexpr int KR = RING ? 32 : 64;           // reduction rows per stage
   // waves: 2 x 2 (64x64 or 32x64 per wave) up to BMG = 128; 4 x 2 of 64x64 for BMG = 256, which
   // halves the B (activation gather) loads and their per-row address math per MFMA
   static constexpr int WAVES_M = BMG == 256 ? 4 : 2;
@@ -1178,8 +1384,8 @@ struct TnCfg {
   static constexpr int WAVES = WAVES_M * WAVES_N;
   static constexpr int NT = 64 * WAVES;
   static constexpr int A_ROWB = BMG * 2;              // bytes per m row of the dy tile image
-  static constexpr int A_BYTES = 64 * A_ROWB;
-  static constexpr int B_BYTES = 64 * 256;            // [64 m][128 col], 256-B rows
+  static constexpr int A_BYTES = KR * A_ROWB;
+  static constexpr int B_BYTES = KR * 256;            // [KR m][128 col], 256-B rows
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int SMEM = STAGES * STAGE;
   static constexpr int TM = BMG / WAVES_M / 16;
@@ -1203,9 +1409,9 @@ constexpr int tn_threads() { return BMG == 256 ? 512 : 256; }  // == TnCfg<BMG, 
 // PW: pointwise conv (1x1, stride 1, no padding): the x row of reduction index m IS pixel m, so a
 // B offset is m*C*2 + channel bytes -- no pixel decomposition, no bounds test (rows past the end
 // fall outside the buffer and read 0).
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW>
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING = false>
 __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
-  using CFG = TnCfg<BMG, BNG, STAGES>;
+  using CFG = TnCfg<BMG, BNG, STAGES, RING>;
   static_assert(CFG::NT == tn_threads<BMG>(), "launch bounds");
   constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1272,7 +1478,7 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
   auto issue = [&](int step, int buf) {
     char* As = smem + buf * CFG::STAGE;
     char* Bs = As + CFG::A_BYTES;
-    const int mb = step * 64;
+    const int mb = step * CFG::KR;
     const int abase = mb * P.Kout * 2;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i)
@@ -1322,9 +1528,43 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
     return base + swz256(row, col >> 3) + ((col & 7) << 1);
   };
 
+  constexpr int LPS = A_PW + B_PW;
+  if constexpr (RING) {
+    // K32 slots j0 .. j0+nj-1; slot j lives in ring buffer j % 4.  Iteration j: wait for slot j
+    // (slots j+1, j+2 may stay in flight), barrier (RAW for slot j; WAR for buffer (j+3) % 4 =
+    // (j-1) % 4, read in iteration j-1 and retired by each wave's lgkmcnt before the barrier),
+    // then refill that buffer with slot j+3 and compute slot j.
+    const int j0 = s_begin * 2, nj = (s_end - s_begin) * 2;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      if (p < nj) issue(j0 + p, p);
+    for (int j = 0; j < nj; ++j) {
+      wait_steps<LPS>(min(nj - 1, j + 2) - j);
+      lds_barrier_rd();
+      if (j + 3 < nj) issue(j0 + j + 3, (j + 3) & 3);
+      const char* As = smem + (j & 3) * CFG::STAGE;
+      const char* Bs = As + CFG::A_BYTES;
+      const int rowA = 8 * g + tq;
+      v4i af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int col = wm * TM * 16 + i * 16 + 4 * tp;
+        af[i] = cat_frag(ds_read_tr(frag_a(As, rowA, col)), ds_read_tr(frag_a(As, rowA + 4, col)));
+      }
+#pragma unroll
+      for (int jj = 0; jj < TN; ++jj) {
+        int col = wn * TN * 16 + jj * 16 + 4 * tp;
+        bfr[jj] = cat_frag(ds_read_tr(frag_b(Bs, rowA, col)), ds_read_tr(frag_b(Bs, rowA + 4, col)));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
+    }
+    lds_barrier_rd();  // every wave's last fragment reads retired before the staging writes
+  } else {
   // STAGES-1 K-steps in flight ahead of the one being consumed; the buffer refilled at the top of
   // iteration i is the one consumed in iteration i-1 (released by that iteration's barrier).
-  constexpr int LPS = A_PW + B_PW;
   const int nst = s_end - s_begin;
 #pragma unroll
   for (int p = 0; p < STAGES - 1; ++p)
@@ -1364,6 +1604,7 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
     cur = cur + 1 == STAGES ? 0 : cur + 1;
     nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
   }
+  }  // !RING
 
   // epilogue: lane holds rows fq*4+e, column fr.  ATOMIC: fp32 atomic add into the zeroed dW
   // (16 lanes = 64 contiguous bytes per row; split count bounded so atomic bytes stay small);
@@ -1681,6 +1922,32 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
   check_launch("igemm_nt");
 }
 
+// The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
+// C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
+static bool ntq_mode() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_NTQ");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+template <int EPI>
+static void run_ntq(const NtArgs& a, hipStream_t st) {
+  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
+  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
+  auto kfn = igemm_ntq_kernel<EPI>;
+  constexpr int smem = CFG::PIPE_BYTES > CFG::EPI_BYTES ? CFG::PIPE_BYTES : CFG::EPI_BYTES;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(512), smem, st, a);
+  check_launch("igemm_ntq");
+}
+
 template <int WM, int WN, int TM, int TN, int EPI>
 static void run_nt_halo(const NtArgs& a, hipStream_t st) {
   using CFG = NtCfg<WM, WN, TM, TN, 2>;
@@ -1847,6 +2114,12 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     else if (rows == 256) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
     else run_nt<2, 2, 4, 4, 2, C64, EPI, OP>(a, st);
     return;
+  }
+  if constexpr (C64 && OP == OP_BF16) {
+    if (rows == 256 && ntq_mode()) {
+      run_ntq<EPI>(a, st);
+      return;
+    }
   }
   const bool k32ok = C64 || !a.c8;  // the 8-channel (stem) loader packs 8 taps per K64 step
   if (a.Nout <= 64) {
@@ -2043,6 +2316,17 @@ static int tn_stages(int bmg) {
   return bmg == 64 ? st64 : st128;
 }
 
+// K32-slot ring for the 64- and 128-row TN tiles (TnCfg RING); PDT_TN_RING=0 restores the
+// two-stage K64 loop (A/B knob)
+static bool tn_ring() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_TN_RING");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 struct WgradPlan {
   int bmg, bng, tiles, splits, steps_per_split, nsteps;
 };
@@ -2099,10 +2383,10 @@ size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
   return (size_t)p.splits * s.K * s.R * s.S * s.C;
 }
 
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW = false>
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW = false, bool RING = false>
 static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
-  using CFG = TnCfg<BMG, BNG, STAGES>;
-  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC, PW>;
+  using CFG = TnCfg<BMG, BNG, STAGES, RING>;
+  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC, PW, RING>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
@@ -2197,13 +2481,23 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
+  const bool ring = tn_ring() && p.bmg != 256 && !deep;
+  const int kr = ring ? 32 : 64;  // reduction rows per pipeline stage
   a.Ho = s.Ho;
-  a.adv_r = 64 % s.Wo;
-  a.adv_qh = (64 / s.Wo) % s.Ho;
-  a.adv_qn = (64 / s.Wo) / s.Ho;
+  a.adv_r = kr % s.Wo;
+  a.adv_qh = (kr / s.Wo) % s.Ho;
+  a.adv_qn = (kr / s.Wo) / s.Ho;
   const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 &&
                   s.H == s.Ho && s.W == s.Wo;
-  if (pw && !deep && p.bmg != 256) {
+  if (ring) {
+    if (p.bmg == 64) {
+      if (pw) { if (atomic) run_tn<64, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
+      else { if (atomic) run_tn<64, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
+    } else {
+      if (pw) { if (atomic) run_tn<128, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
+      else { if (atomic) run_tn<128, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
+    }
+  } else if (pw && !deep && p.bmg != 256) {
     if (p.bmg == 64) { if (atomic) run_tn<64, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false, true>(a, p.tiles, p.splits, st); }
     else { if (atomic) run_tn<128, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 2, false, true>(a, p.tiles, p.splits, st); }
   } else if (p.bmg == 256) {

@@ -59,6 +59,10 @@ def _bacc(p, c):
         p._pdt_bacc = a
     return a
 _FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
+# test hook (tests/test_blocks_gpu.py, mask-matched reference): when a list, every fused block
+# forward appends its units' stored post-activation outputs (z, NHWC bf16), so an fp32 reference
+# can take the native path's ReLU decisions and compare gradients without ReLU-flip noise
+_CAPTURE = None
 _COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
 
 
@@ -884,6 +888,8 @@ class _ResidualBlock(torch.autograd.Function):
             h = z
         if holder is not None and h8 is not None:
             holder.append(h8)
+        if _CAPTURE is not None:
+            _CAPTURE.append([z for z, _, _ in outs])
         for ui, (z, y, stt) in enumerate(outs):
             saved += [z, y, stt]
             _nan_trace(f"fwd block{id(ctx) % 10007} unit{ui} {tuple(y.shape)}", z=z, y=y, stats=stt)

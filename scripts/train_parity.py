@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Training-level parity: the native bf16 path vs the stock fp32 path, same init, same data.
 
-Trains ResNet-18 (the reference model, resnet/main.py:76) on a learnable synthetic CIFAR-shaped
-set (class templates + noise, ``data.learnable_dataset``) with the reference optimizer
+Trains ResNet-18 (the reference model, resnet/main.py:76; ``--arch resnet50 --image 112`` for the
+headline model) on a learnable synthetic CIFAR-shaped set (class templates + noise, ``data.learnable_dataset``) with the reference optimizer
 (SGD lr 0.01, momentum 0.9, wd 1e-5, resnet/main.py:103) for ``--steps`` steps:
 
 * native: our NHWC bf16 kernels, our DDP wrapper (world 1: flat buffers, in-place gradient
@@ -55,15 +55,18 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--window", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--arch", default="resnet18")
+    ap.add_argument("--image", type=int, default=32, help="image side (32: CIFAR-shaped)")
+    ap.add_argument("--classes", type=int, default=10)
     ap.add_argument("--fp8", action="store_true",
                     help="native side on the fp8 path (e4m3 activations / e5m2 gradients, fp8 wgrad)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.fp8:
         ops.set_fp8(True)
-    ds = learnable_dataset(a.samples, 32, 10, device=dev, seed=3, noise=a.noise)
+    ds = learnable_dataset(a.samples, a.image, a.classes, device=dev, seed=3, noise=a.noise)
     torch.manual_seed(0)
-    stock = build_model("resnet18", num_classes=10).to(dev)
+    stock = build_model(a.arch, num_classes=a.classes).to(dev)
     native_m = copy.deepcopy(stock).set_impl("native")
     native = DistributedDataParallel(native_m)          # world 1: flat space + grad sinks
     opt_n = SGD(native.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
@@ -94,6 +97,7 @@ def main():
     w = a.window
     nwin = a.steps // w
     res = {
+        "arch": a.arch, "image": a.image, "fp8": bool(a.fp8),
         "steps": a.steps, "batch": a.batch, "samples": a.samples, "noise": a.noise, "lr": a.lr,
         "window": w,
         "native_window_loss": [round(float(ln[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],
