@@ -36,7 +36,19 @@ def _run(fault=None, timeout=5.0, nproc=2):
            "--timeout", str(timeout)]
     t0 = time.time()
     r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=240, capture_output=True, text=True)
-    res = [json.loads(l[len("RESULT "):]) for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    # both ranks print through one pipe: under load their lines can interleave, so decode every
+    # "RESULT " payload with raw_decode instead of assuming one JSON object per line
+    dec, res, pos = json.JSONDecoder(), [], 0
+    while True:
+        pos = r.stdout.find("RESULT ", pos)
+        if pos < 0:
+            break
+        try:
+            obj, end = dec.raw_decode(r.stdout, pos + len("RESULT "))
+            res.append(obj)
+            pos = end
+        except json.JSONDecodeError:
+            pos += len("RESULT ")
     return r, {x["rank"]: x for x in res}, time.time() - t0
 
 
