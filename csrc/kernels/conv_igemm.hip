@@ -1111,7 +1111,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
 // 1-block-per-CU 256x256 tile that step is ~1 us -- about one L2->LDS DMA latency under load, so
 // long-K GEMMs stall once per step (4096^3: 642 TF/s vs hipBLASLt 1,524).
 //
-// This kernel splits each 64-deep K-step of the 256x256 tile into FOUR phases, one per output
+// This kernel splits each 64-deep K-step of the 256x256 (or 128x128) tile into FOUR phases, one per output
 // quadrant (X half hx, W half hw), so a quarter tile (one half of one operand, 16 KB) is dead as
 // soon as its last phase has read it, and is refilled right then with the same quarter of step
 // s+2 (two LDS stages, 128 KB):
@@ -1137,18 +1137,38 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
 // an asm barrier)
 __device__ __forceinline__ void lds_barrier_rd() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int EPI>
-__global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
-  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
-  static_assert(CFG::BM == 256 && CFG::BN == 256 && CFG::NT == 512, "ntq geometry");
-  constexpr int EB = 2, KE = 64, QB = 16384;  // quarter: 128 rows x 128 B
+// Geometry: WM x WN waves, each owning a contiguous (2*TMQ*16) x (2*TNQ*16) output tile made of
+// its four quadrant sub-tiles (TMQ x TNQ MFMA tiles each).  256x256: 8 waves (2 x 4), TMQ 4,
+// TNQ 2 (one block per CU, 128 KB of LDS).  128x128: 4 waves (2 x 2), TMQ = TNQ = 2 (64 KB, two
+// blocks per CU).  A quarter is always BM/2 (or BN/2) rows x 128 B = 2 DMA pieces per wave.
+template <int WM, int WN, int TMQ, int TNQ>
+struct NtqCfg {
+  static constexpr int WAVES = WM * WN, NT = WAVES * 64;
+  static constexpr int BM = WM * TMQ * 32, BN = WN * TNQ * 32;
+  static constexpr int QX = BM / 2 * 128, QW = BN / 2 * 128;  // quarter bytes
+  static constexpr int STAGE = 2 * QX + 2 * QW;
+  static_assert(QX == WAVES * 2048 && QW == WAVES * 2048, "a quarter is two 1-KiB DMA pieces per wave");
+  using Epi = NtCfg<WM, WN, 2 * TMQ, 2 * TNQ, 2, false>;
+  static constexpr int SMEM = 2 * STAGE > Epi::EPI_BYTES ? 2 * STAGE : Epi::EPI_BYTES;
+  static constexpr int MIN_WAVES = WAVES == 8 ? 1 : 2;  // waves per SIMD: 1 or 2 blocks per CU
+};
+
+template <int WM, int WN, int TMQ, int TNQ, int EPI>
+__global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_WAVES))
+    igemm_ntq_kernel(const NtArgs P) {
+  using Q = NtqCfg<WM, WN, TMQ, TNQ>;
+  using CFG = typename Q::Epi;
+  constexpr int BM = Q::BM, BN = Q::BN, QX = Q::QX, QW = Q::QW, STAGE = Q::STAGE;
+  constexpr int HX = BM / WM / 2, HW = BN / WN / 2;  // rows of one wave's quadrant sub-tile
+  static_assert(CFG::BM == BM && CFG::BN == BN, "ntq geometry");
+  constexpr int EB = 2, KE = 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int ntn = (P.Nout + 255) / 256;
-  const int ntm = (P.M + 255) / 256;
+  const int ntn = (P.Nout + BN - 1) / BN;
+  const int ntm = (P.M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, ntm * ntn);
   const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
-  const int m0 = tmi * 256, n0 = tni * 256;
+  const int m0 = tmi * BM, n0 = tni * BN;
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -1156,7 +1176,9 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
 
-  // this lane's DMA rows: piece i (0, 1) of half h covers half-local rows r = (wid*2 + i)*8 + lr
+  // this lane's DMA rows: piece i (0, 1) of half h covers half-local rows r = (wid*2 + i)*8 + lr;
+  // half-local row r of X half h is GEMM row (r / HX)*2*HX + h*HX + r % HX (wave-row blocks), of W
+  // half h channel (r / HW)*2*HW + h*HW + r % HW
   int a_base[2][2], b_row[2][2], b_c[2][2];
   uint32_t a_inv[2][2];
 #pragma unroll
@@ -1166,7 +1188,7 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
       const int r = (wid * 2 + i) * 8 + lr;
       const int sc = lj ^ ((r >> 1) & 7);  // source chunk landing in slot lj (read side: swz128)
       b_c[h][i] = sc;
-      const int m = m0 + (r >> 6) * 128 + h * 64 + (r & 63);
+      const int m = m0 + (r / HX) * 2 * HX + h * HX + (r % HX);
       int pix = 0, h0 = -(1 << 20), w0 = 0;
       if (m < P.M) {
         const uint32_t n = fdiv((uint32_t)m, P.div_ij);
@@ -1190,7 +1212,7 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
       uint32_t spread = 0u;
       for (int ti = 0; ti < nr; ++ti) spread |= ((hm >> ti) & 1u) << (ti * ns);
       a_inv[h][i] = ~(wmk * spread);
-      const int ch = n0 + (r >> 5) * 64 + h * 32 + (r & 31);
+      const int ch = n0 + (r / HW) * 2 * HW + h * HW + (r % HW);
       b_row[h][i] = ch < P.Nout ? ch * P.Kg : -1;
     }
 
@@ -1208,7 +1230,7 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
   // quarter (operand X = 0 / W = 1, half h) of the step held by the tracker, into stage `st`
   auto issue = [&](int op, int h, int st) {
     const bool valid = q_kt < nk;
-    char* dst = smem + st * 65536 + (op * 2 + h) * QB + wid * 2048;
+    char* dst = smem + st * STAGE + (op == 0 ? h * QX : 2 * QX + h * QW) + wid * 2048;
     if (op == 0) {
       const int tap = q_ti * P.tns + q_tj;
       const int dr = P.dr0 + q_ti * P.dstep, ds = P.ds0 + q_tj * P.dstep;
@@ -1229,13 +1251,13 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
     }
   };
 
-  const int wm = wid % 2, wn = wid / 2;
+  const int wm = wid % WM, wn = wid / WM;
   const int fr = lane & 15, fq = lane >> 4;
-  v4f acc[8][4];
+  v4f acc[2 * TMQ][2 * TNQ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * TMQ; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2 * TNQ; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   // prologue: steps 0 and 1, every quarter in consumption order (X0, W0, W1, X1)
 #pragma unroll
@@ -1243,64 +1265,64 @@ __global__ void __launch_bounds__(512, 1) igemm_ntq_kernel(const NtArgs P) {
     issue(0, 0, st); issue(1, 0, st); issue(1, 1, st); issue(0, 1, st);
     advance();
   }
-  // fragments: X rows of this wave in a half = wm*64 + i*16 + fr (4 tiles); W rows = wn*32 + j*16 + fr
-  auto read_x = [&](const char* base, v4i (&f)[4][2]) {
+  // fragments: X rows of this wave in a half = wm*HX + i*16 + fr; W rows = wn*HW + j*16 + fr
+  auto read_x = [&](const char* base, v4i (&f)[TMQ][2]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        f[i][ks] = *reinterpret_cast<const v4i*>(base + swz128(wm * 64 + i * 16 + fr, ks * 4 + fq));
-  };
-  auto read_w = [&](const char* base, v4i (&f)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < TMQ; ++i)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        f[j][ks] = *reinterpret_cast<const v4i*>(base + swz128(wn * 32 + j * 16 + fr, ks * 4 + fq));
+        f[i][ks] = *reinterpret_cast<const v4i*>(base + swz128(wm * HX + i * 16 + fr, ks * 4 + fq));
   };
-  auto mma = [&](int i0, int j0, const v4i (&xf)[4][2], const v4i (&wf)[2][2]) {
+  auto read_w = [&](const char* base, v4i (&f)[TNQ][2]) {
+#pragma unroll
+    for (int j = 0; j < TNQ; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        f[j][ks] = *reinterpret_cast<const v4i*>(base + swz128(wn * HW + j * 16 + fr, ks * 4 + fq));
+  };
+  auto mma = [&](int i0, int j0, const v4i (&xf)[TMQ][2], const v4i (&wf)[TNQ][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i0 + i][j0 + j] = mfma16(wf[j][ks], xf[i][ks], acc[i0 + i][j0 + j]);
+        for (int j = 0; j < TNQ; ++j) acc[i0 + i][j0 + j] = mfma16(wf[j][ks], xf[i][ks], acc[i0 + i][j0 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
-  v4i x0[4][2], x1[4][2], w0f[2][2], w1f[2][2];
+  v4i x0[TMQ][2], x1[TMQ][2], w0f[TNQ][2], w1f[TNQ][2];
   for (int s = 0; s < nk; ++s) {
     const int st = s & 1;
-    const char* base = smem + st * 65536;
+    const char* base = smem + st * STAGE;
     // P0: Q(0,0)
     wait_vm<12>();
     lds_barrier_rd();
     read_x(base, x0);
-    read_w(base + 2 * QB, w0f);
+    read_w(base + 2 * QX, w0f);
     mma(0, 0, x0, w0f);
     // P1: Q(0,1); X0 and W0 of this stage are dead -> refill with step s+2
     wait_vm<10>();
     lds_barrier_rd();
     issue(0, 0, st);
     issue(1, 0, st);
-    read_w(base + 3 * QB, w1f);
-    mma(0, 2, x0, w1f);
+    read_w(base + 2 * QX + QW, w1f);
+    mma(0, TNQ, x0, w1f);
     // P2: Q(1,0); W1 dead
     wait_vm<12>();
     lds_barrier_rd();
     issue(1, 1, st);
-    read_x(base + QB, x1);
-    mma(4, 0, x1, w0f);
+    read_x(base + QX, x1);
+    mma(TMQ, 0, x1, w0f);
     // P3: Q(1,1) from registers; X1 dead
     lds_barrier_rd();
     issue(0, 1, st);
     advance();
-    mma(4, 2, x1, w1f);
+    mma(TMQ, TNQ, x1, w1f);
   }
   wait_vm<0>();
-  lds_barrier();  // every DMA landed and every fragment read done before the epilogue reuses LDS
-  nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, m0, n0, tmi);
+  lds_barrier_rd();  // every DMA landed and every fragment read done before the epilogue reuses LDS
+  nt_epilogue<CFG, WM, WN, 2 * TMQ, 2 * TNQ, EPI, OP_BF16>(P, acc, smem, m0, n0, tmi);
 }
 
 // ============================================================================
@@ -1924,27 +1946,28 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 
 // The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
-static bool ntq_mode() {
+// PDT_NTQ: bit 0 = the 256x256 tile, bit 1 = the 128x128 tile (default 1: the 128x128 tile keeps
+// its 2-stage loop until measured; 3 = both, 0 = neither)
+static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PDT_NTQ");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = e ? atoi(e) : 1;
   }
-  return v == 1;
+  return v;
 }
 
-template <int EPI>
+template <int WM, int WN, int TMQ, int TNQ, int EPI>
 static void run_ntq(const NtArgs& a, hipStream_t st) {
-  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
-  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
-  auto kfn = igemm_ntq_kernel<EPI>;
-  constexpr int smem = CFG::PIPE_BYTES > CFG::EPI_BYTES ? CFG::PIPE_BYTES : CFG::EPI_BYTES;
+  using Q = NtqCfg<WM, WN, TMQ, TNQ>;
+  const int ntm = (a.M + Q::BM - 1) / Q::BM, ntn = (a.Nout + Q::BN - 1) / Q::BN;
+  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, Q::SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(512), smem, st, a);
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(Q::NT), Q::SMEM, st, a);
   check_launch("igemm_ntq");
 }
 
@@ -2116,8 +2139,12 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     return;
   }
   if constexpr (C64 && OP == OP_BF16) {
-    if (rows == 256 && ntq_mode()) {
-      run_ntq<EPI>(a, st);
+    if (rows == 256 && (ntq_mode() & 1)) {
+      run_ntq<2, 4, 4, 2, EPI>(a, st);
+      return;
+    }
+    if (rows == 128 && (ntq_mode() & 2) && a.Nout > 64 && !use_mid_tile(a.M, a.Nout, a.Kg * 2)) {
+      run_ntq<2, 2, 2, 2, EPI>(a, st);
       return;
     }
   }

@@ -14,6 +14,7 @@
 #   pmc:<counters>[:args]  one rocprofv3 --pmc pass over bench.py <args>          -> gpurun_out/TAG_pmc_N
 #   py:<script>[:args]     python -u <script> <args>
 #   pmcpy:<ctrs>:<script>[:args]  one rocprofv3 --pmc pass over python <script> <args>  -> TAG_pmc_N
+#   exe:<binary>[:args]    a program built in-tree beforehand (e.g. build/prio_repro)
 #   env:VAR=VALUE          export VAR for the steps after it (env:VAR= unsets it)
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -71,6 +72,9 @@ for st in "$@"; do
     py)
       s=${rest%%:*}; args=""; [ "$s" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       run "py_$(basename "$s" .py)" 900 python -u "$s" $args || exit 1 ;;
+    exe)
+      b=${rest%%:*}; args=""; [ "$b" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
+      run "exe_$(basename "$b")" 300 "./$b" $args || exit 1 ;;
     env)
       var=${rest%%=*}; val=${rest#*=}
       if [ -n "$val" ]; then export "$var=$val"; else unset "$var"; fi
