@@ -1,5 +1,7 @@
 #include "rccl_comm.h"
 
+#include "stream_sync.h"
+
 #include <c10/hip/HIPGuard.h>
 
 #include <condition_variable>
@@ -378,14 +380,12 @@ ncclRedOp_t RcclComm::op_of(const std::string& op) {
 
 void RcclComm::comm_wait_current() {
   hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream();
-  hip_check(hipEventRecord(ev_a_, cur), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(stream(), ev_a_, 0), "hipStreamWaitEvent");
+  stream_handoff(cur, stream(), ev_a_);
 }
 
 void RcclComm::current_wait_comm() {
   hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream();
-  hip_check(hipEventRecord(ev_b_, stream()), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(cur, ev_b_, 0), "hipStreamWaitEvent");
+  stream_handoff(stream(), cur, ev_b_);
 }
 
 void RcclComm::synchronize() {

@@ -1,5 +1,7 @@
 #include "xgmi_comm.h"
 
+#include "stream_sync.h"
+
 #include <c10/hip/HIPGuard.h>
 
 #include <chrono>
@@ -174,14 +176,12 @@ void XgmiComm::reduce_bucket_phases(int bucket, int64_t offset, int64_t count, b
 
 void XgmiComm::comm_wait_current() {
   hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream();
-  hipc(hipEventRecord(ev_a_, cur), "hipEventRecord");
-  hipc(hipStreamWaitEvent(stream(), ev_a_, 0), "hipStreamWaitEvent");
+  stream_handoff(cur, stream(), ev_a_);
 }
 
 void XgmiComm::current_wait_comm() {
   hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream();
-  hipc(hipEventRecord(ev_b_, stream()), "hipEventRecord");
-  hipc(hipStreamWaitEvent(cur, ev_b_, 0), "hipStreamWaitEvent");
+  stream_handoff(stream(), cur, ev_b_);
 }
 
 void XgmiComm::synchronize() {

@@ -1,5 +1,7 @@
 #include "reducer.h"
 
+#include "../comm/stream_sync.h"
+
 #include <c10/hip/HIPGuard.h>
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/function.h>
@@ -78,8 +80,7 @@ struct ReducerState {
       c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
       xgmi->comm_wait_current();
       if (aux) {
-        hipEventRecord(ev_aux, aux);
-        hipStreamWaitEvent(xgmi->stream(), ev_aux, 0);
+        stream_handoff(aux, xgmi->stream(), ev_aux);
       }
       if (timing && first) hipEventRecord(ev_start, xgmi->stream());
       xgmi->reduce_bucket((int)b, flat_off[b], flats[b].numel(), average);
@@ -92,8 +93,7 @@ struct ReducerState {
       comm->comm_wait_current();
       hipStream_t cs = comm->stream();
       if (aux) {
-        hipEventRecord(ev_aux, aux);
-        hipStreamWaitEvent(cs, ev_aux, 0);
+        stream_handoff(aux, cs, ev_aux);
       }
       if (timing && first) hipEventRecord(ev_start, cs);
       if (wire_bf16) {
