@@ -1409,7 +1409,10 @@ struct TnCfg {
   static constexpr int A_BYTES = KR * A_ROWB;
   static constexpr int B_BYTES = KR * 256;            // [KR m][128 col], 256-B rows
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int SMEM = STAGES * STAGE;
+  // RING at BMG 256 (one 8-wave block per CU either way): room for the staged epilogue's
+  // wave-private row images too (8 waves x 64 rows x 64 fp32)
+  static constexpr int STAGED_BYTES = WAVES * (BMG / WAVES_M) * 64 * 4;
+  static constexpr int SMEM = (RING && BMG == 256 && STAGED_BYTES > STAGES * STAGE) ? STAGED_BYTES : STAGES * STAGE;
   static constexpr int TM = BMG / WAVES_M / 16;
   static constexpr int TN = BNG / WAVES_N / 16;
   static constexpr int A_LPR = A_ROWB / 16;           // lanes per row in one 1-KiB DMA instruction
@@ -2508,7 +2511,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   const int64_t n = (int64_t)s.K * a.Ncols;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
   const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
-  const bool ring = tn_ring() && p.bmg != 256 && !deep;
+  const bool ring = tn_ring() && !deep;
   const int kr = ring ? 32 : 64;  // reduction rows per pipeline stage
   a.Ho = s.Ho;
   a.adv_r = kr % s.Wo;
@@ -2517,7 +2520,10 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 &&
                   s.H == s.Ho && s.W == s.Wo;
   if (ring) {
-    if (p.bmg == 64) {
+    if (p.bmg == 256) {  // PDT_TN_WIDE=1: 8-wave 256x128 tile, one block per CU
+      if (pw) { if (atomic) run_tn<256, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<256, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
+      else { if (atomic) run_tn<256, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<256, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
+    } else if (p.bmg == 64) {
       if (pw) { if (atomic) run_tn<64, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
       else { if (atomic) run_tn<64, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
     } else {
