@@ -251,7 +251,7 @@ __device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
 // shortcut of a downsampling block.  It is normalised here and rounded to bf16 exactly as a
 // separate apply pass would have stored it, so the block output is bit-identical to the unfused
 // path while the normalised shortcut is never written or read back (2 x |shortcut| of HBM).
-template <bool RES, bool RELU, bool MASK = false, bool RESBN = false>
+template <bool RES, bool RELU, bool MASK = false, bool RESBN = false, int U = 1>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
@@ -272,10 +272,10 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
     load8(rscale + c0, rsc);
     load8(rshift + c0, rsh);
   }
-  for (int64_t v = v0; v < nvec; v += stride) {
-    f8 a = unpack8(y[v]);
+  auto body = [&](int64_t v, const uint4 yv, const uint4 rv) {
+    f8 a = unpack8(yv);
     f8 r;
-    if (RES) r = unpack8(res[v]);
+    if (RES) r = unpack8(rv);
     if constexpr (RESBN) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) r.v[j] = bf2f(f2bf(fmaf(r.v[j], rsc[j], rsh[j])));
@@ -296,7 +296,23 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
       for (int j = 0; j < 8; ++j) bits |= (zr.v[j] > 0.f ? 1u : 0u) << j;
       zmask[v] = (uint8_t)bits;
     }
+  };
+  int64_t v = v0;
+  if constexpr (U > 1) {
+    // U vectors per thread per iteration: every load of the batch is issued before the first
+    // store (the compiler cannot hoist a load above a store that may alias it)
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+      uint4 yv[U], rv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        yv[u] = y[v + u * stride];
+        if (RES) rv[u] = res[v + u * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(v + u * stride, yv[u], RES ? rv[u] : yv[u]);
+    }
   }
+  for (; v < nvec; v += stride) body(v, y[v], RES ? res[v] : uint4{});
 }
 
 // grid of an 8-channel-vector elementwise pass: at most kEwCap (kEwCapResidual for the residual
@@ -318,12 +334,45 @@ static int ew_block_cap_env() {
 constexpr int kEwCap = 8192;
 constexpr int kEwCapResidual = 32768;
 
+// PDT_EW_UNROLL = U (1, 2 or 4): the bn_act_fwd / bn_bwd_apply passes keep U 16-byte vectors of
+// every operand in flight per thread (loads batched ahead of the math and the stores), on a grid
+// of at most one resident wave per slot (2048 blocks).  Default 1: the round-3 grid-stride form.
+static int ew_unroll() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_EW_UNROLL");
+    v = e ? atoi(e) : 1;
+    v = (v == 2 || v == 4) ? v : 1;
+  }
+  return v;
+}
+
 static int ew_blocks(int64_t nvec, int K8, int cap_default = kEwCap) {
+  if (ew_unroll() > 1) cap_default = 2048;  // resident blocks of 256 threads (8 per CU)
   int64_t b = (nvec + 255) / 256;
   const int64_t cap = ew_block_cap_env() > 0 ? ew_block_cap_env() : cap_default;
   b = b < cap ? b : cap;
   const int64_t q = K8 / std::gcd(K8, 256);
   return (int)(((b + q - 1) / q) * q);
+}
+
+template <bool RES, bool RELU, bool MASK, bool RESBN>
+static void fwd_launch(dim3 g, dim3 b, hipStream_t st, const uint4* Y, const float* scale, const float* shift,
+                       const uint4* R, uint4* Z, int64_t nvec, int K8, uint8_t* zmask = nullptr,
+                       const float* rscale = nullptr, const float* rshift = nullptr) {
+  switch (ew_unroll()) {
+    case 4:
+      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 4>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+                         zmask, rscale, rshift);
+      break;
+    case 2:
+      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 2>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+                         zmask, rscale, rshift);
+      break;
+    default:
+      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 1>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+                         zmask, rscale, rshift);
+  }
 }
 
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
@@ -339,27 +388,27 @@ void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift
     if (!res || !rshift) throw std::runtime_error("bn_act_fwd: residual BN needs the residual and its shift");
     if (zmask) {
       if (!relu) throw std::runtime_error("bn_act_fwd: a ReLU mask needs relu");
-      hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+      fwd_launch<true, true, true, true>(g, b, st, Y, scale, shift, R, Z, nvec, K8,
                          zmask, rscale, rshift);
     } else if (relu) {
-      hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, false, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec,
+      fwd_launch<true, true, false, true>(g, b, st, Y, scale, shift, R, Z, nvec,
                          K8, nullptr, rscale, rshift);
     } else {
-      hipLaunchKernelGGL((bn_act_fwd_kernel<true, false, false, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec,
+      fwd_launch<true, false, false, true>(g, b, st, Y, scale, shift, R, Z, nvec,
                          K8, nullptr, rscale, rshift);
     }
     return;
   }
   if (zmask) {
     if (!relu) throw std::runtime_error("bn_act_fwd: a ReLU mask needs relu");
-    if (res) hipLaunchKernelGGL((bn_act_fwd_kernel<true, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8, zmask);
-    else hipLaunchKernelGGL((bn_act_fwd_kernel<false, true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8, zmask);
+    if (res) fwd_launch<true, true, true, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8, zmask);
+    else fwd_launch<false, true, true, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8, zmask);
   } else if (res) {
-    if (relu) hipLaunchKernelGGL((bn_act_fwd_kernel<true, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
-    else hipLaunchKernelGGL((bn_act_fwd_kernel<true, false>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
+    if (relu) fwd_launch<true, true, false, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8);
+    else fwd_launch<true, false, false, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_act_fwd_kernel<false, true>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
-    else hipLaunchKernelGGL((bn_act_fwd_kernel<false, false>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8);
+    if (relu) fwd_launch<false, true, false, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8);
+    else fwd_launch<false, false, false, false>(g, b, st, Y, scale, shift, R, Z, nvec, K8);
   }
 }
 
@@ -601,7 +650,7 @@ void launch_bn_act_bwd_reduce(const uint16_t* dz, const uint16_t* z, const uint1
 // Grid-stride with gridDim*256 a multiple of K/8, so every thread keeps one fixed 8-channel
 // group: the per-channel coefficients are computed once per thread, not per element.
 // Q8: also dy8 = e5m2(bf16(dy) * s_t) with delayed scaling (fp8_util.h) for an fp8 dgrad
-template <int MASK, bool TRAIN, bool DRES, bool Q8 = false>
+template <int MASK, bool TRAIN, bool DRES, bool Q8 = false, int U = 1>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const uint4* __restrict__ dz, const uint4* __restrict__ z, const uint4* __restrict__ y,
     const float* __restrict__ stats, const float* __restrict__ gamma,
@@ -642,11 +691,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       }
     }
   }
-  for (int64_t v = tid; v < nvec; v += stride) {
-    f8 d = unpack8(dz[v]);
+  auto body = [&](int64_t v, const uint4 dv, const uint4 zv, const uint4 yv) {
+    f8 d = unpack8(dv);
     f8 zz, yy;
-    if (MASK == 1) zz = unpack8(z[v]);
-    if (TRAIN || MASK == 2) yy = unpack8(y[v]);
+    if (MASK == 1) zz = unpack8(zv);
+    if (TRAIN || MASK == 2) yy = unpack8(yv);
     f8 o, gr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -668,7 +717,23 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
       }
       dy8[v] = make_uint2(cvt4_e5m2(t[0], t[1], t[2], t[3]), cvt4_e5m2(t[4], t[5], t[6], t[7]));
     }
+  };
+  constexpr bool RZ = MASK == 1, RY = TRAIN || MASK == 2;
+  int64_t v = tid;
+  if constexpr (U > 1) {  // U vectors of every operand in flight before the first store
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+      uint4 dv[U], zv[U], yv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        dv[u] = dz[v + u * stride];
+        if (RZ) zv[u] = z[v + u * stride];
+        if (RY) yv[u] = y[v + u * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(v + u * stride, dv[u], RZ ? zv[u] : dv[u], RY ? yv[u] : dv[u]);
+    }
   }
+  for (; v < nvec; v += stride) body(v, dz[v], RZ ? z[v] : uint4{}, RY ? y[v] : uint4{});
   if constexpr (Q8) block_amax(qm, state + slot * SLOT_FLOATS);
 }
 
@@ -685,9 +750,16 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   auto DY = reinterpret_cast<uint4*>(dy);
   auto DR = reinterpret_cast<uint4*>(dres);
   float invM = 1.f / (float)M;
-#define PDT_BWD(MK, TR, DRS)                                                                  \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, TR, DRS>), g, b, 0, st, DZ, Z, Y, stats, gamma, \
+  const int unr = ew_unroll();
+#define PDT_BWD_U(MK, TR, DRS, UU)                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, TR, DRS, false, UU>), g, b, 0, st, DZ, Z, Y, stats, gamma, \
                      sums, nvec, K8, invM, DY, DR, nullptr, nullptr, 0, dgamma, dbeta)
+#define PDT_BWD(MK, TR, DRS)                                            \
+  do {                                                                  \
+    if (unr == 4) PDT_BWD_U(MK, TR, DRS, 4);                            \
+    else if (unr == 2) PDT_BWD_U(MK, TR, DRS, 2);                       \
+    else PDT_BWD_U(MK, TR, DRS, 1);                                     \
+  } while (0)
 #define PDT_BWD_T(MK)                                                             \
   if (training) { if (dres) PDT_BWD(MK, true, true); else PDT_BWD(MK, true, false); } \
   else { if (dres) PDT_BWD(MK, false, true); else PDT_BWD(MK, false, false); }
@@ -696,6 +768,7 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   else { PDT_BWD_T(0) }
 #undef PDT_BWD_T
 #undef PDT_BWD
+#undef PDT_BWD_U
 }
 
 void launch_bn_act_bwd_apply_q8(const uint16_t* dz, const uint16_t* z, const uint16_t* y,

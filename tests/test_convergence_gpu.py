@@ -54,3 +54,28 @@ def test_two_ranks_stay_bit_identical_while_training(gpu, tmp_path):
     for h in hist:  # every checkpoint: both ranks' parameter checksums equal
         assert h[0] == h[1], hist
     assert res[0]["learn_loss"][-1] < res[0]["learn_loss"][0], res[0]["learn_loss"]
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
+    """the headline model, ResNet-50 at 112 px, batch 64, 200 steps on the
+    learnable set, native bf16 (and the fp8 path: e4m3 forward, e5m2 gradients, fp8 weight
+    gradients) against stock fp32 from the same init; same window criterion as above."""
+    out = tmp_path / "parity50.json"
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_parity.py"), "--arch", "resnet50",
+                        "--image", "112", "--batch", "64", "--samples", "2048", "--steps", "200",
+                        "--json", str(out)] + (["--fp8"] if fp8 else []), cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=230)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["finite"] and res["arch"] == "resnet50" and res["image"] == 112
+    n, s = res["native_window_loss"], res["stock_window_loss"]
+    if os.environ.get("PDT_REPORT_DIR"):
+        with open(os.path.join(os.environ["PDT_REPORT_DIR"], "resnet50_parity.txt"), "a") as f:
+            f.write(json.dumps(res) + "\n")
+    # both learn (the loss falls well below its start), and track each other window by window
+    assert n[-1] < 0.5 * n[0] and s[-1] < 0.5 * s[0], (n, s)
+    for a, b in zip(n, s):
+        assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)

@@ -347,6 +347,8 @@ def test_bn_single_launch_reductions_match_two_launch_and_grid_caps(gpu):
     small = _run_bn({"PDT_EW_BLOCKS": "256"})      # many grid-stride iterations per thread
     assert base == two, "last-block handshake differs from the two-launch reduction"
     assert base == small, "capped grid-stride passes differ from the default grids"
+    for u in ("2", "4"):  # PDT_EW_UNROLL: U vectors per thread in flight, resident-size grids
+        assert base == _run_bn({"PDT_EW_UNROLL": u}), f"unrolled ({u}) BN passes differ"
     # every reduction two-level (no single-block direct finish): same statistics within fp32
     # rounding of the different summation tree
     tree = _run_bn({"PDT_FIN_SINGLE": "0"})
