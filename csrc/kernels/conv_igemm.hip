@@ -1153,7 +1153,9 @@ struct NtqCfg {
   static constexpr int MIN_WAVES = WAVES == 8 ? 1 : 2;  // waves per SIMD: 1 or 2 blocks per CU
 };
 
-template <int WM, int WN, int TMQ, int TNQ, int EPI>
+// OP: bf16 (a 128-B K-step = 64 elements = two 16x16x32 MFMAs per tile pair) or fp8 (128
+// elements = one MX-rate 16x16x128 MFMA, operand = 32 B per lane: chunks 2fq, 2fq+1)
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
 __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_WAVES))
     igemm_ntq_kernel(const NtArgs P) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
@@ -1161,7 +1163,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   constexpr int BM = Q::BM, BN = Q::BN, QX = Q::QX, QW = Q::QW, STAGE = Q::STAGE;
   constexpr int HX = BM / WM / 2, HW = BN / WN / 2;  // rows of one wave's quadrant sub-tile
   static_assert(CFG::BM == BM && CFG::BN == BN, "ntq geometry");
-  constexpr int EB = 2, KE = 64;
+  constexpr int EB = OP == OP_BF16 ? 2 : 1, KE = 128 / EB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Nout + BN - 1) / BN;
@@ -1265,29 +1267,45 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
     issue(0, 0, st); issue(1, 0, st); issue(1, 1, st); issue(0, 1, st);
     advance();
   }
-  // fragments: X rows of this wave in a half = wm*HX + i*16 + fr; W rows = wn*HW + j*16 + fr
+  // fragments: X rows of this wave in a half = wm*HX + i*16 + fr; W rows = wn*HW + j*16 + fr.
+  // A fragment holds the two 16-B chunks this lane feeds to one K-step's MFMAs: bf16 -- chunk fq
+  // (k-sub-step 0) and 4 + fq (k-sub-step 1); fp8 -- chunks 2fq, 2fq+1 of the 16x16x128 operand
+  auto read_frag = [&](const char* base, int row, v4i (&f)[2]) {
+    if constexpr (OP == OP_BF16) {
+      f[0] = *reinterpret_cast<const v4i*>(base + swz128(row, fq));
+      f[1] = *reinterpret_cast<const v4i*>(base + swz128(row, 4 + fq));
+    } else {
+      f[0] = *reinterpret_cast<const v4i*>(base + swz128(row, 2 * fq));
+      f[1] = *reinterpret_cast<const v4i*>(base + swz128(row, 2 * fq + 1));
+    }
+  };
   auto read_x = [&](const char* base, v4i (&f)[TMQ][2]) {
 #pragma unroll
-    for (int i = 0; i < TMQ; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        f[i][ks] = *reinterpret_cast<const v4i*>(base + swz128(wm * HX + i * 16 + fr, ks * 4 + fq));
+    for (int i = 0; i < TMQ; ++i) read_frag(base, wm * HX + i * 16 + fr, f[i]);
   };
   auto read_w = [&](const char* base, v4i (&f)[TNQ][2]) {
 #pragma unroll
-    for (int j = 0; j < TNQ; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        f[j][ks] = *reinterpret_cast<const v4i*>(base + swz128(wn * HW + j * 16 + fr, ks * 4 + fq));
+    for (int j = 0; j < TNQ; ++j) read_frag(base, wn * HW + j * 16 + fr, f[j]);
   };
   auto mma = [&](int i0, int j0, const v4i (&xf)[TMQ][2], const v4i (&wf)[TNQ][2]) {
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (OP == OP_BF16) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) acc[i0 + i][j0 + j] = mfma16(wf[j][ks], xf[i][ks], acc[i0 + i][j0 + j]);
+    } else {
 #pragma unroll
       for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-        for (int j = 0; j < TNQ; ++j) acc[i0 + i][j0 + j] = mfma16(wf[j][ks], xf[i][ks], acc[i0 + i][j0 + j]);
+        for (int j = 0; j < TNQ; ++j) {
+          const v8i a8 = __builtin_shufflevector(wf[j][0], wf[j][1], 0, 1, 2, 3, 4, 5, 6, 7);
+          const v8i b8 = __builtin_shufflevector(xf[i][0], xf[i][1], 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[i0 + i][j0 + j] = mfma_f8<OP>(a8, b8, acc[i0 + i][j0 + j]);
+        }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -1322,7 +1340,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   }
   wait_vm<0>();
   lds_barrier_rd();  // every DMA landed and every fragment read done before the epilogue reuses LDS
-  nt_epilogue<CFG, WM, WN, 2 * TMQ, 2 * TNQ, EPI, OP_BF16>(P, acc, smem, m0, n0, tmi);
+  nt_epilogue<CFG, WM, WN, 2 * TMQ, 2 * TNQ, EPI, OP>(P, acc, smem, m0, n0, tmi);
 }
 
 // ============================================================================
@@ -1949,8 +1967,8 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 
 // The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
-// PDT_NTQ: bit 0 = the 256x256 tile, bit 1 = the 128x128 tile (default 1: the 128x128 tile keeps
-// its 2-stage loop until measured; 3 = both, 0 = neither)
+// PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
+// tile (default 1: the others keep their 2-stage loops until measured; 7 = all, 0 = none)
 static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
@@ -1960,11 +1978,11 @@ static int ntq_mode() {
   return v;
 }
 
-template <int WM, int WN, int TMQ, int TNQ, int EPI>
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
 static void run_ntq(const NtArgs& a, hipStream_t st) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
   const int ntm = (a.M + Q::BM - 1) / Q::BM, ntn = (a.Nout + Q::BN - 1) / Q::BN;
-  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI>;
+  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI, OP>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, Q::SMEM);
@@ -2135,6 +2153,12 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     }
   }
   if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
+    if constexpr (C64) {
+      if (rows == 256 && (ntq_mode() & 4)) {  // PDT_NTQ bit 2: the quadrant-phased fp8 256x256 tile
+        run_ntq<2, 4, 4, 2, EPI, OP>(a, st);
+        return;
+      }
+    }
     if (a.Nout <= 64) run_nt<4, 1, 4, 4, 2, C64, EPI, OP>(a, st);
     else if (rows == 64) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
     else if (rows == 256) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
