@@ -25,16 +25,15 @@ namespace {
 // one 64-bit signal slot per producer stream, in signal memory of the producer's device
 struct Slots {
   std::mutex mu;
-  std::unordered_map<int, uint64_t*> base;             // device -> 256 slots
-  std::unordered_map<hipStream_t, int> slot_of;        // producer stream -> slot index
+  // producer stream -> its 8-byte signal word (hipMallocSignalMemory allocates one word at a
+  // time), allocated on the device current at its first hand-off
+  std::unordered_map<hipStream_t, uint64_t*> slot_of;
   std::unordered_map<hipStream_t, uint64_t> ticket;    // last ticket written by that producer
-  std::unordered_map<int, int> used;                   // device -> slots handed out
 };
 Slots& slots() {
   static Slots s;
   return s;
 }
-constexpr int kSlots = 256;
 }  // namespace
 
 static bool capturing(hipStream_t s) {
@@ -54,24 +53,16 @@ void stream_handoff(hipStream_t producer, hipStream_t consumer, hipEvent_t ev) {
   uint64_t* ptr;
   uint64_t t;
   {
-    int dev = 0;
-    sync_check(hipGetDevice(&dev), "hipGetDevice");
-    auto b = S.base.find(dev);
-    if (b == S.base.end()) {
-      uint64_t* p = nullptr;
-      sync_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&p), kSlots * sizeof(uint64_t), hipMallocSignalMemory),
-                 "hipExtMallocWithFlags(signal)");
-      sync_check(hipMemset(p, 0, kSlots * sizeof(uint64_t)), "hipMemset");
-      sync_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-      b = S.base.emplace(dev, p).first;
-    }
     auto it = S.slot_of.find(producer);
     if (it == S.slot_of.end()) {
-      int& u = S.used[dev];
-      if (u >= kSlots) throw std::runtime_error("stream_handoff: out of signal slots");
-      it = S.slot_of.emplace(producer, u++).first;
+      uint64_t* p = nullptr;
+      sync_check(hipExtMallocWithFlags(reinterpret_cast<void**>(&p), sizeof(uint64_t), hipMallocSignalMemory),
+                 "hipExtMallocWithFlags(signal)");
+      sync_check(hipMemset(p, 0, sizeof(uint64_t)), "hipMemset");
+      sync_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+      it = S.slot_of.emplace(producer, p).first;
     }
-    ptr = b->second + it->second;
+    ptr = it->second;
     t = ++S.ticket[producer];
   }
   sync_check(hipStreamWriteValue64(producer, ptr, t, 0), "hipStreamWriteValue64");

@@ -2154,7 +2154,7 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
   }
   if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
     if constexpr (C64) {
-      if (rows == 256 && (ntq_mode() & 4)) {  // PDT_NTQ bit 2: the quadrant-phased fp8 256x256 tile
+      if (rows == 256 && a.Nout > 64 && (ntq_mode() & 4)) {  // PDT_NTQ bit 2: quadrant-phased fp8 256x256
         run_ntq<2, 4, 4, 2, EPI, OP>(a, st);
         return;
       }
@@ -2166,7 +2166,7 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     return;
   }
   if constexpr (C64 && OP == OP_BF16) {
-    if (rows == 256 && (ntq_mode() & 1)) {
+    if (rows == 256 && a.Nout > 64 && (ntq_mode() & 1)) {  // (Nout <= 64 is the 256x64 tile)
       run_ntq<2, 4, 4, 2, EPI>(a, st);
       return;
     }
@@ -2370,13 +2370,15 @@ static int tn_stages(int bmg) {
   return bmg == 64 ? st64 : st128;
 }
 
-// K32-slot ring for the 64- and 128-row TN tiles (TnCfg RING); PDT_TN_RING=0 restores the
-// two-stage K64 loop (A/B knob)
+// K32-slot ring for the TN tiles (TnCfg RING), PDT_TN_RING=1.  Off by default: measured slower
+// on MI355X (r4b, bench_conv.py, same call): ResNet-50 wgrad total 5.77 ms with the ring vs 4.74
+// ms with the two-stage K64 loop -- a barrier (and lgkmcnt drain) per 16 MFMAs per wave costs
+// more than the deeper load lead gains.
 static bool tn_ring() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PDT_TN_RING");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = (e && e[0] == '1') ? 1 : 0;
   }
   return v == 1;
 }

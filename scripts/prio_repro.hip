@@ -46,9 +46,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bufB, 256 * 256 * sizeof(float)));
   CK(hipMemset(bufA, 0, 256 * 256 * sizeof(float)));
   CK(hipMemset(bufB, 0, 256 * 256 * sizeof(float)));
-  uint64_t* flags = nullptr;  // [0]: A -> B sequence, [1]: B -> A sequence
-  CK(hipExtMallocWithFlags((void**)&flags, 2 * sizeof(uint64_t), hipMallocSignalMemory));
-  CK(hipMemset(flags, 0, 2 * sizeof(uint64_t)));
+  // [0]: A -> B sequence, [1]: B -> A sequence; signal memory is allocated one 8-byte word at a
+  // time (hipMallocSignalMemory refuses larger sizes on MI355X / ROCm 7.2)
+  uint64_t* fl[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; ++i) {
+    CK(hipExtMallocWithFlags((void**)&fl[i], sizeof(uint64_t), hipMallocSignalMemory));
+    CK(hipMemset(fl[i], 0, sizeof(uint64_t)));
+  }
   int wv = 0;
   CK(hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, 0));
   printf("priority range least %d greatest %d; stream wait value supported: %d\n", lo, hi, wv);
@@ -79,16 +83,16 @@ int main(int argc, char** argv) {
                 CK(hipEventRecord(ea, A));
                 CK(hipStreamWaitEvent(B, ea, 0));
               } else {
-                CK(hipStreamWriteValue64(A, flags, seq, 0));
-                CK(hipStreamWaitValue64(B, flags, seq, hipStreamWaitValueGte, ~0ull));
+                CK(hipStreamWriteValue64(A, fl[0], seq, 0));
+                CK(hipStreamWaitValue64(B, fl[0], seq, hipStreamWaitValueGte, ~0ull));
               }
               hipLaunchKernelGGL(small_kernel, dim3(64), dim3(256), 0, B, bufB, 100);
               if (sy == EVENT) {
                 CK(hipEventRecord(eb, B));
                 CK(hipStreamWaitEvent(A, eb, 0));
               } else {
-                CK(hipStreamWriteValue64(B, flags + 1, seq, 0));
-                CK(hipStreamWaitValue64(A, flags + 1, seq, hipStreamWaitValueGte, ~0ull));
+                CK(hipStreamWriteValue64(B, fl[1], seq, 0));
+                CK(hipStreamWaitValue64(A, fl[1], seq, hipStreamWaitValueGte, ~0ull));
               }
             }
           }
@@ -113,6 +117,7 @@ int main(int argc, char** argv) {
       }
   CK(hipFree(bufA));
   CK(hipFree(bufB));
-  CK(hipFree(flags));
+  CK(hipFree(fl[0]));
+  CK(hipFree(fl[1]));
   return 0;
 }
