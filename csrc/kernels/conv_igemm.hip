@@ -1155,7 +1155,7 @@ struct NtqCfg {
 
 // OP: bf16 (a 128-B K-step = 64 elements = two 16x16x32 MFMAs per tile pair) or fp8 (128
 // elements = one MX-rate 16x16x128 MFMA, operand = 32 B per lane: chunks 2fq, 2fq+1)
-template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16, bool PIPE = false>
 __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_WAVES))
     igemm_ntq_kernel(const NtArgs P) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
@@ -1310,6 +1310,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   };
 
   v4i x0[TMQ][2], x1[TMQ][2], w0f[TNQ][2], w1f[TNQ][2];
+  if constexpr (!PIPE) {
   for (int s = 0; s < nk; ++s) {
     const int st = s & 1;
     const char* base = smem + st * STAGE;
@@ -1337,6 +1338,47 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
     issue(0, 1, st);
     advance();
     mma(TMQ, TNQ, x1, w1f);
+  }
+  } else {
+  // PIPE: every phase's fragment reads are issued one phase EARLY, right after that phase's
+  // barrier, and land while this phase's MFMAs run (the reads of a phase no longer wait behind
+  // its own barrier):  P0 reads W1(s) | P1 reads X1(s) | P2 none | P3 reads X0, W0 of step s+1
+  // (x0 / w0f are dead after P1 / P2).  Waits per phase (glds younger than the quarters read):
+  // P0 W1(s): 10, P1 X1(s): 8, P3 X0, W0(s+1): 10.  Refills as above (X0, W0 at P1, W1 at P2, X1
+  // at P3); each refill's slot was last read one phase earlier, retired by that phase's barrier.
+  wait_vm<12>();
+  lds_barrier_rd();
+  read_x(smem, x0);
+  read_w(smem + 2 * QX, w0f);
+  for (int s = 0; s < nk; ++s) {
+    const int st = s & 1;
+    const char* base = smem + st * STAGE;
+    const char* nbase = smem + (st ^ 1) * STAGE;
+    // P0: Q(0,0) from x0 / w0f; read W1(s)
+    wait_vm<10>();
+    lds_barrier_rd();
+    read_w(base + 2 * QX + QW, w1f);
+    mma(0, 0, x0, w0f);
+    // P1: Q(0,1); X0, W0 slots (read at P3 of step s-1) -> step s+2; read X1(s)
+    wait_vm<8>();
+    lds_barrier_rd();
+    issue(0, 0, st);
+    issue(1, 0, st);
+    read_x(base + QX, x1);
+    mma(0, TNQ, x0, w1f);
+    // P2: Q(1,0); W1 slot (read at P0) -> step s+2
+    lds_barrier_rd();
+    issue(1, 1, st);
+    mma(TMQ, 0, x1, w0f);
+    // P3: Q(1,1); X1 slot (read at P1) -> step s+2; read X0, W0 of step s+1
+    wait_vm<10>();
+    lds_barrier_rd();
+    issue(0, 1, st);
+    advance();
+    read_x(nbase, x0);
+    read_w(nbase + 2 * QX, w0f);
+    mma(TMQ, TNQ, x1, w1f);
+  }
   }
   wait_vm<0>();
   lds_barrier_rd();  // every DMA landed and every fragment read done before the epilogue reuses LDS
@@ -1968,7 +2010,8 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 // The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
 // PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
-// tile (default 1: the others keep their 2-stage loops until measured; 7 = all, 0 = none)
+// tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile (default 1: the others keep
+// their 2-stage loops until measured; 7 = all tiles, 0 = none)
 static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
@@ -1978,11 +2021,11 @@ static int ntq_mode() {
   return v;
 }
 
-template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16, bool PIPE = false>
 static void run_ntq(const NtArgs& a, hipStream_t st) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
   const int ntm = (a.M + Q::BM - 1) / Q::BM, ntn = (a.Nout + Q::BN - 1) / Q::BN;
-  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI, OP>;
+  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI, OP, PIPE>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, Q::SMEM);
@@ -2170,7 +2213,8 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
   }
   if constexpr (C64 && OP == OP_BF16) {
     if (rows == 256 && a.Nout > 64 && (ntq_mode() & 1)) {  // (Nout <= 64 is the 256x64 tile)
-      run_ntq<2, 4, 4, 2, EPI>(a, st);
+      if (ntq_mode() & 8) run_ntq<2, 4, 4, 2, EPI, OP_BF16, true>(a, st);
+      else run_ntq<2, 4, 4, 2, EPI>(a, st);
       return;
     }
     if (rows == 128 && (ntq_mode() & 2) && a.Nout > 64 && !use_mid_tile(a.M, a.Nout, a.Kg * 2)) {

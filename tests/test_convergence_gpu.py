@@ -64,8 +64,11 @@ def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
     out = tmp_path / "parity50.json"
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    # lr 0.004: at the reference's 0.01 ResNet-50 on this set spikes to loss ~8 in the first 20
+    # steps in BOTH runs (stock included) and the windows are chaotic; at 0.004 both fit the set
+    # (r4d: native 2.57 -> 0.062, stock 2.57 -> 0.097, train acc 0.999 / 0.996)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_parity.py"), "--arch", "resnet50",
-                        "--image", "112", "--batch", "64", "--samples", "2048", "--steps", "200",
+                        "--image", "112", "--batch", "64", "--lr", "0.004", "--steps", "200",
                         "--json", str(out)] + (["--fp8"] if fp8 else []), cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=230)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -76,6 +79,7 @@ def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
         with open(os.path.join(os.environ["PDT_REPORT_DIR"], "resnet50_parity.txt"), "a") as f:
             f.write(json.dumps(res) + "\n")
     # both learn (the loss falls well below its start), and track each other window by window
-    assert n[-1] < 0.5 * n[0] and s[-1] < 0.5 * s[0], (n, s)
+    assert n[-1] < 0.2 * n[0] and s[-1] < 0.2 * s[0], (n, s)
+    assert res["native_train_acc"] > 0.9 and res["stock_train_acc"] > 0.9, res
     for a, b in zip(n, s):
         assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)
