@@ -15,6 +15,9 @@ print(f"step span {(t1 - t0) / 1000:.1f} us, {len(step)} kernels")
 
 def family(n):
     n = n.split("(")[0].replace("void ", "").replace("pdt::", "")
+    if "igemm_ntq_kernel" in n:  # <WM, WN, TMQ, TNQ, EPI, OP, PIPE>
+        args = n.split("<")[1].split(">")[0].split(",")
+        return f"ntq epi{args[4].strip()} op{args[5].strip() if len(args) > 5 else '0'}"
     for key in ("igemm_nt_kernel", "igemm_tn_kernel", "bn_bwd_apply", "bn_act_fwd", "bn_finalize",
                 "bn_bwd_part", "bn_bwd_reduce", "quant", "pool_bn", "fc_gemm", "sgd", "pack"):
         if key in n:
