@@ -33,7 +33,9 @@ __global__ void small_kernel(float* p, int iters) {
   p[i] = v;
 }
 
-enum Sync { NONE = 0, EVENT = 1, VALUE = 2 };
+enum Sync { NONE = 0, EVENT = 1, VALUE = 2, ONEWAY = 3 };
+// ONEWAY: the reducer's pattern during backward -- A records an event every PERIOD kernels, B
+// waits for it and runs its kernel, but A never waits for B (until the end of the run)
 
 int main(int argc, char** argv) {
   const int nk = argc > 1 ? atoi(argv[1]) : 400;      // kernels on stream A per run
@@ -57,11 +59,11 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, 0));
   printf("priority range least %d greatest %d; stream wait value supported: %d\n", lo, hi, wv);
   printf("%-8s %-8s %-6s %10s %10s\n", "A_prio", "B_prio", "sync", "us/kernel", "min");
-  const char* sname[] = {"none", "event", "value"};
+  const char* sname[] = {"none", "event", "value", "oneway"};
   uint64_t seq = 0;
   for (int pa = 0; pa < 2; ++pa)
     for (int pb = 0; pb < 2; ++pb)
-      for (int sy = 0; sy < 3; ++sy) {
+      for (int sy = 0; sy < 4; ++sy) {
         if (sy == VALUE && !wv) continue;
         hipStream_t A, B;
         CK(hipStreamCreateWithPriority(&A, hipStreamNonBlocking, pa ? hi : lo));
@@ -79,7 +81,7 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(small_kernel, dim3(256), dim3(256), 0, A, bufA, 200);
             if (sy != NONE && (k + 1) % period == 0) {
               ++seq;
-              if (sy == EVENT) {
+              if (sy == EVENT || sy == ONEWAY) {
                 CK(hipEventRecord(ea, A));
                 CK(hipStreamWaitEvent(B, ea, 0));
               } else {
@@ -87,7 +89,8 @@ int main(int argc, char** argv) {
                 CK(hipStreamWaitValue64(B, fl[0], seq, hipStreamWaitValueGte, ~0ull));
               }
               hipLaunchKernelGGL(small_kernel, dim3(64), dim3(256), 0, B, bufB, 100);
-              if (sy == EVENT) {
+              if (sy == ONEWAY) {
+              } else if (sy == EVENT) {
                 CK(hipEventRecord(eb, B));
                 CK(hipStreamWaitEvent(A, eb, 0));
               } else {
@@ -95,6 +98,10 @@ int main(int argc, char** argv) {
                 CK(hipStreamWaitValue64(A, fl[1], seq, hipStreamWaitValueGte, ~0ull));
               }
             }
+          }
+          if (sy == ONEWAY) {  // join B once at the end
+            CK(hipEventRecord(eb, B));
+            CK(hipStreamWaitEvent(A, eb, 0));
           }
           CK(hipEventRecord(e1, A));
           CK(hipEventSynchronize(e1));
