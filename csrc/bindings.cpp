@@ -1381,6 +1381,7 @@ PYBIND11_MODULE(_C, m) {
     const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
     return out.narrow(0, 0, got);
   }, py::arg("n"));
+  m.def("conv_stream_k_launches", []() { return pdt::conv_stream_k_launches(); });
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);

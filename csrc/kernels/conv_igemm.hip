@@ -33,16 +33,20 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace pdt {
 
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------- utilities
 struct FastDiv {  // n / d for 0 <= n < 2^31 via mul-hi
@@ -1386,6 +1390,308 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
 }
 
 // ============================================================================
+//        NT 256x256, ping-pong wave groups (long-K fwd / dgrad, bf16)
+// ============================================================================
+// Two wave groups share every SIMD (waves w and w+4; G0 = waves 0-3, G1 = waves 4-7) and run the
+// same program one segment apart, so while one wave of a SIMD issues its MFMAs the other issues
+// its LDS-DMA pieces and fragment reads (MI355X_MICROARCH "Two waves per SIMD"; the structure of
+// the 256x256 8-phase template in cdna_hip_programming.md 5):
+//     wave:  L_0 | C_0 | L_1 | C_1 | ...        (| = workgroup barrier)
+//     G0     L   | C   | L   | C   | ...
+//     G1     -   | L   | C   | L   | C ...      (one extra barrier before its first segment)
+// A segment works on one K32 half-step m (32 channels of one tap): L_m issues this wave's 4 DMA
+// pieces of half m+3 into ring slot (m+3) % 4 (= slot m-1, read by both groups' L_{m-1}, which
+// are both behind this L in barrier order), reads the wave's 12 fragments of half m, and waits
+// (vmcnt 8: halves m+2, m+3 may stay in flight) for its own pieces of half m+1 before the
+// barrier; C_m runs the wave's 32 MFMAs.  RAW: half m+1 is read first by G0's L_{m+1}, one
+// barrier after BOTH groups' L_m waits.  Every half is issued 3 L-segments (~4 MFMA segments of
+// the SIMD) before its first read.  Slots: [X 256 rows x 64 B][W 256 rows x 64 B] = 32 KB, 4 slots.
+// Wave tiles as igemm_ntq's epilogue wants them: (wm = wid % 2) 128 rows x (wn = wid / 2) 64 cols.
+// K64 = true: K64 steps in 2 stages of [X 256 x 128 B][W 256 x 128 B] (full 128-B rows: one global
+// line per row), segments = the two k-sub-steps of a step.  L(k, 0) (k >= 1) issues step k+1 into
+// stage (k+1) & 1 = (k-1) & 1 (last read by G1's L(k-1, 1), one barrier earlier); L(k, 1) ends
+// with vmcnt(0) for it, so a piece has ~3 segments to land instead of ~5 (K32 ring).
+// Stream-K (SK = true), for grids of fewer 256x256 tiles than CUs (the long-K 3x3 / 1x1 shapes of
+// the 14x14 and 7x7 stages: 196 and 98 tiles on 256 CUs).  The (tile, K-unit) iteration space,
+// tile-major, is cut into gridDim.x equal contiguous ranges, one per workgroup.  A range starts
+// with the tail of one tile (unless it starts on a tile boundary), continues over whole tiles and
+// ends with the head of another.  The workgroup that runs a tile's first unit owns the tile: it
+// adds the fp32 partial sums of the workgroups whose ranges start inside the tile (in workgroup
+// order: deterministic) and runs the normal epilogue.  A contributor stores its partial once, in
+// its own 256 KB workspace slot (lane-native order: one float4 per lane and accumulator tile),
+// publishes it (device-scope stores, vmcnt(0), barrier, flag = 1); the owner polls each flag,
+// resets it to 0 (the next launch starts from zeros, also under graph replay) and reads the slot
+// with device-scope loads.  Owners wait
+// only on HIGHER workgroup ids, whose partial is the FIRST thing they compute; every workgroup is
+// resident at once (grid <= CUs, one workgroup per CU), so the waits end.
+// Partials cross XCDs (each XCD has its own L2): contributors store and owners load them with the
+// device-scope cache policy (SC1), so no L2-wide writeback / invalidate is needed around the flags.
+constexpr int kCpolSc1 = 16;
+constexpr int kSkMaxParts = 2;  // partials one owner adds (the launcher keeps per_wg >= nu / 2)
+
+struct NtpSk {
+  float* ws;          // [gridDim.x][8 waves][32 tiles][64 lanes][4]
+  uint32_t* flags;    // [gridDim.x]
+  int per_wg;         // K-units per workgroup range
+  uint32_t ws_bytes;
+};
+
+template <int EPI, bool K64, bool SK>
+__global__ void __launch_bounds__(512, 1) igemm_ntp_kernel(const NtArgs P, const NtpSk S) {
+  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
+  static_assert(CFG::BM == 256 && CFG::BN == 256, "ntp geometry");
+  constexpr int EB = 2;
+  constexpr int ROWB = K64 ? 128 : 64;     // bytes per tile row in LDS
+  constexpr int KH = ROWB / EB;            // channels per DMA unit (step or half)
+  constexpr int SLOT = 2 * 256 * ROWB;     // 64 KB stage / 32 KB half slot
+  constexpr int NSLOT = K64 ? 2 : 4;
+  constexpr int LPR = ROWB / 16, RPP = 64 / LPR;  // lanes per row, rows per 1-KiB piece
+  constexpr int PP = 256 / RPP / 8;               // pieces per operand per wave: 4 (K64) / 2 (K32)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int ntn = (P.Nout + 255) / 256;
+  const int ntm = (P.M + 255) / 256;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool g1 = wid >= 4;
+  const int lr = lane / LPR, lj = lane % LPR;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
+  auto rd_off = [](int row, int chunk) {
+    if constexpr (K64) return swz128(row, chunk);
+    else return swz64(row, chunk);
+  };
+  const int upc = P.CA / KH;               // units per tap
+  const int nu = P.ntaps * upc;            // units per tile
+  const int wm = wid % 2, wn = wid / 2;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // units [ub, ue) of tile (tmi, tni) into acc (which the caller zeroed)
+  auto tile_loop = [&](int m0, int n0, int ub, int ue, v4f (&acc)[8][4]) {
+    // this lane's DMA rows: piece p covers tile rows r = (wid*PP + p)*RPP + lr of X and of W
+    int a_base[PP], b_row[PP], b_c[PP];
+    uint32_t a_inv[PP];
+#pragma unroll
+    for (int p = 0; p < PP; ++p) {
+      const int r = (wid * PP + p) * RPP + lr;
+      const int sc = K64 ? (lj ^ ((r >> 1) & 7)) : (lj ^ swz64_g(r));  // source chunk landing in slot lj
+      b_c[p] = sc;
+      const int m = m0 + r;
+      int pix = 0, h0 = -(1 << 20), w0 = 0;
+      if (m < P.M) {
+        const uint32_t n = fdiv((uint32_t)m, P.div_ij);
+        const uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
+        const uint32_t ii = fdiv(rem, P.div_j);
+        const uint32_t jj = rem - ii * (uint32_t)P.Mj;
+        pix = (int)n * P.HA * P.WA;
+        h0 = (int)ii * P.ash + P.aoff_h;
+        w0 = (int)jj * P.asw + P.aoff_w;
+      }
+      a_base[p] = (pix + h0 * P.WA + w0) * P.CA * EB + sc * 16;
+      const int nr = P.tnr, ns = P.tns;
+      const int hb = h0 + P.dr0, wb = w0 + P.ds0;
+      const int hlo = P.dstep > 0 ? max(0, -hb) : max(0, hb - P.HA + 1);
+      const int hhi = P.dstep > 0 ? min(nr, P.HA - hb) : min(nr, hb + 1);
+      const int wlo = P.dstep > 0 ? max(0, -wb) : max(0, wb - P.WA + 1);
+      const int whi = P.dstep > 0 ? min(ns, P.WA - wb) : min(ns, wb + 1);
+      const uint32_t hm = hhi > hlo ? (1u << (hhi & 31)) - (1u << (hlo & 31)) : 0u;
+      const uint32_t wmk = whi > wlo ? (1u << (whi & 31)) - (1u << (wlo & 31)) : 0u;
+      uint32_t spread = 0u;
+      for (int ti = 0; ti < nr; ++ti) spread |= ((hm >> ti) & 1u) << (ti * ns);
+      a_inv[p] = ~(wmk * spread);
+      const int ch = n0 + r;
+      b_row[p] = ch < P.Nout ? ch * P.Kg : -1;
+    }
+
+    // state of the NEXT unit to issue: tap row, tap column, channel offset, unit index
+    const int tap0 = ub / upc;
+    int q_ti = tap0 / P.tns, q_tj = tap0 - (tap0 / P.tns) * P.tns, q_chb = (ub - tap0 * upc) * KH;
+    int q_u = 0;  // relative to ub
+    const int n_u = ue - ub;
+    auto issue_next = [&]() {
+      const bool valid = q_u < n_u;
+      char* slot = smem + (q_u % NSLOT) * SLOT;
+      const int tap = q_ti * P.tns + q_tj;
+      const int dr = P.dr0 + q_ti * P.dstep, ds = P.ds0 + q_tj * P.dstep;
+      const int tdelta = ((dr * P.WA + ds) * P.CA + q_chb) * EB;
+      const int tbo = ((P.tr0 + q_ti * P.tstep) * P.S + (P.ts0 + q_tj * P.tstep)) * P.CA + q_chb;
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[p], (unsigned)tap, 1u) |
+                                (valid ? 0u : 0xffffffffu);
+        glds16(ra, slot + (wid * PP + p) * 1024, (uint32_t)(a_base[p] + tdelta) | poison);
+      }
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const uint32_t off = (valid && b_row[p] >= 0) ? (uint32_t)((b_row[p] + tbo) * EB + b_c[p] * 16) : OOB;
+        glds16(rb, slot + SLOT / 2 + (wid * PP + p) * 1024, off);
+      }
+      ++q_u;
+      q_chb += KH;
+      if (q_chb == P.CA) {
+        q_chb = 0;
+        if (++q_tj == P.tns) { q_tj = 0; ++q_ti; }
+      }
+    };
+
+    // prologue: K64 -- units 0, 1; K32 -- halves 0, 1, 2.  Unit 0 landed everywhere before the reads.
+    issue_next();
+    issue_next();
+    if constexpr (!K64) issue_next();
+    wait_vm<K64 ? 2 * PP : 4 * PP>();
+    lds_barrier_rd();
+    if (g1) {
+      __builtin_amdgcn_s_setprio(1);  // the younger group: static priority (MI355X_MICROARCH item 4)
+      lds_barrier();                  // one segment behind G0
+    }
+    const int nh = K64 ? 2 * n_u : n_u;  // segments
+    v4i xf[8], wf[4];
+    for (int m = 0; m < nh; ++m) {
+      // L_m
+      const char* xs;
+      int ck;
+      if constexpr (K64) {
+        const int k = m >> 1, ks = m & 1;
+        if (ks == 0 && k >= 1) issue_next();  // unit k + 1
+        xs = smem + (k & 1) * SLOT;
+        ck = ks * 4 + fq;
+      } else {
+        issue_next();  // half m + 3 into slot (m + 3) % 4
+        xs = smem + (m & 3) * SLOT;
+        ck = fq;
+      }
+      const char* ws = xs + SLOT / 2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xf[i] = *reinterpret_cast<const v4i*>(xs + rd_off(wm * 128 + i * 16 + fr, ck));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[j] = *reinterpret_cast<const v4i*>(ws + rd_off(wn * 64 + j * 16 + fr, ck));
+      if constexpr (K64) {
+        if (m & 1) wait_vm<0>();  // this wave's pieces of unit k + 1
+      } else {
+        wait_vm<4 * PP>();  // this wave's pieces of half m + 1
+      }
+      // the segment boundaries are scheduling fences: without them the compiler interleaves the
+      // fragment reads with the MFMAs and hoists most MFMAs above the barrier (into L), which
+      // undoes the ping-pong
+      __builtin_amdgcn_sched_barrier(0);
+      lds_barrier_rd();  // fragments in registers; the next unit visible to the next L
+      __builtin_amdgcn_sched_barrier(0);
+      // C_m
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(wf[j], xf[i], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      lds_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (!g1) lds_barrier();  // G1 took its extra barrier at the start: equal counts
+    wait_vm<0>();
+    lds_barrier_rd();  // every DMA landed and every fragment read done before LDS is reused
+    if (g1) __builtin_amdgcn_s_setprio(0);
+  };
+
+  v4f acc[8][4];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  };
+  if constexpr (!SK) {
+    const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
+    zero();
+    tile_loop(tmi * 256, tni * 256, 0, nu, acc);
+    nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, tmi * 256, tni * 256, tmi);
+  } else {
+    // a range spans at most two tiles (the launcher keeps per_wg <= nu): the segment that starts
+    // it and, when it crosses a tile boundary, the head of the next tile.  Two straight-line
+    // segments rather than a loop: hoisting the lane-invariant address math of the main loop and
+    // of the epilogue out of a loop kept it all live and spilled.
+    const int b = blockIdx.x;
+    const int64_t total = (int64_t)ntm * ntn * nu;
+    const int64_t it0 = (int64_t)b * S.per_wg;
+    const int64_t it1 = min(total, it0 + S.per_wg);
+    auto segment = [&](int tile, int ub, int ue) {
+      const int tmi = tile / ntn, tni = tile - (tile / ntn) * ntn;
+      zero();
+      tile_loop(tmi * 256, tni * 256, ub, ue, acc);
+      if (ub > 0) {
+        // contributor: publish the partial
+        // buffer stores: one lane offset + a scalar offset per accumulator tile (flat addresses
+        // would cost a 64-bit VGPR pair per tile: 31 KB is past the immediate-offset range)
+        const __amdgpu_buffer_rsrc_t rw = make_rsrc(S.ws, S.ws_bytes);
+        const int voff = (wid * 32 * 64 + lane) * 16;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rw, voff,
+                                                   b * 262144 + (i * 4 + j) * 1024, kCpolSc1);
+        wait_vm<0>();  // device-scope stores performed (no L2-wide writeback: buffer_wbl2 per
+        lds_barrier(); // contributor cost 3x in kernel time)
+        if (t == 0) __hip_atomic_store(S.flags + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      // owner: add the partials of the ranges that start inside the tile (at most kSkMaxParts), in
+      // workgroup order.  No branch around the accumulators: thread 0
+      // waits for the flags first, then every candidate is added, a missing one as zeros read
+      // through an out-of-range buffer offset (with acc modified under a branch, the compiler
+      // copied all 128 accumulators at each merge and spilled).
+      int nc = 0;
+      if (ue < nu) {
+        while (nc < kSkMaxParts && (int64_t)(b + nc + 1) * S.per_wg < (int64_t)(tile + 1) * nu) ++nc;
+        if (t == 0) {
+          for (int c = 1; c <= nc; ++c) {
+            // relaxed device-scope polls: an acquire load invalidates the XCD's whole L2 on every
+            // poll; the partials are read below with device-scope loads instead
+            while (__hip_atomic_load(S.flags + b + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+              __builtin_amdgcn_s_sleep(2);
+            __hip_atomic_store(S.flags + b + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        lds_barrier();
+      }
+      {
+        const __amdgpu_buffer_rsrc_t rw = make_rsrc(S.ws, S.ws_bytes);
+        const int lane_off = (wid * 32 * 64 + lane) * 16;
+#pragma unroll
+        for (int c = 1; c <= kSkMaxParts; ++c) {
+          const int voff = c <= nc ? lane_off : (int)OOB;
+          const int soff = (c <= nc ? b + c : 0) * 262144;
+#pragma unroll
+          for (int i = 0; i < 8; i += 2) {
+            v4f v[2][4];
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj)
+                v[ii][jj] = __builtin_bit_cast(
+                    v4f, __builtin_amdgcn_raw_buffer_load_b128(rw, voff, soff + ((i + ii) * 4 + jj) * 1024, kCpolSc1));
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) acc[i + ii][jj] += v[ii][jj];
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, tmi * 256, tni * 256, tmi);
+    };
+    if (it0 >= it1) return;
+    const int tile0 = (int)(it0 / nu);
+    const int ub0 = (int)(it0 - (int64_t)tile0 * nu);
+    const int ue0 = (int)min((int64_t)nu, ub0 + (it1 - it0));
+    segment(tile0, ub0, ue0);
+    if (it0 + (ue0 - ub0) < it1) {
+      lds_barrier();  // the first segment's LDS use (epilogue staging) ends before the next DMA
+      segment(tile0 + 1, 0, (int)(it1 - (int64_t)(tile0 + 1) * nu));
+    }
+  }
+}
+
+// ============================================================================
 //                      TN implicit GEMM (wgrad, split-K)
 // ============================================================================
 struct TnArgs {
@@ -2010,13 +2316,13 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 // The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
 // PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
-// tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile (default 1: the others keep
-// their 2-stage loops until measured; 7 = all tiles, 0 = none)
+// tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile, bit 4 / bit 5 = the
+// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 33 = ping-pong K64; 1 = the quadrant-phased kernel; 0 = none)
 static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PDT_NTQ");
-    v = e ? atoi(e) : 1;
+    v = e ? atoi(e) : 33;  // ping-pong K64 256x256 (r4h: 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899)
   }
   return v;
 }
@@ -2033,6 +2339,133 @@ static void run_ntq(const NtArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(Q::NT), Q::SMEM, st, a);
   check_launch("igemm_ntq");
+}
+
+template <int EPI, bool K64>
+static void run_ntp(const NtArgs& a, hipStream_t st) {
+  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
+  auto kfn = igemm_ntp_kernel<EPI, K64, false>;
+  constexpr int smem = 4 * 32768;  // 2 K64 stages / 4 K32 slots (= the epilogue's staging)
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(512), smem, st, a, NtpSk{nullptr, nullptr, 0, 0});
+  check_launch("igemm_ntp");
+}
+
+// Stream-K workspace: one 256 KB fp32 slot and one flag per workgroup, per (device, stream) --
+// two streams never share flags, so concurrent stream-K GEMMs cannot consume each other's
+// partials.  Flags start at zero and every owner resets the ones it consumed.  Allocated on the
+// first eager launch; a launch under graph capture with no workspace yet falls back to the
+// plain kernel.
+struct SkWorkspace {
+  float* ws = nullptr;
+  uint32_t* flags = nullptr;
+  int slots = 0;
+};
+static SkWorkspace* sk_workspace(hipStream_t st, int slots) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SkWorkspace> all;
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(mu);
+  SkWorkspace& s = all[{dev, st}];
+  if (s.slots >= slots) return &s;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
+  auto ck = [](hipError_t e) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("stream-K workspace: ") + hipGetErrorString(e));
+  };
+  if (s.ws) {
+    ck(hipStreamSynchronize(st));
+    ck(hipFree(s.ws));
+    ck(hipFree(s.flags));
+  }
+  ck(hipMalloc(&s.ws, (size_t)slots * 65536 * sizeof(float)));
+  ck(hipMalloc(&s.flags, (size_t)slots * sizeof(uint32_t)));
+  ck(hipMemsetAsync(s.flags, 0, (size_t)slots * sizeof(uint32_t), st));
+  s.slots = slots;
+  return &s;
+}
+
+static int device_cus() {
+  static int cus[16] = {0};
+  int dev = 0;
+  hipGetDevice(&dev);
+  if (!cus[dev & 15]) {
+    int v = 0;
+    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    cus[dev & 15] = v > 0 ? v : 256;
+  }
+  return cus[dev & 15];
+}
+
+// PDT_NT_SK: 0 = off (default), 1 = stream-K for 256x256-tile grids smaller than the CU count,
+// 2 = force it wherever the 256x256 tile could run (tests).  Measured slower (r4n, one MI355X):
+// 50176x2304->256 672 vs 893 TF isolated (partials cross XCDs through HBM: 256 KB per split tile
+// each way, plus the spilled reduction block), and the ResNet-50 step 40.0 vs 18.9 ms -- owners
+// spin on CUs while the side-stream wgrad kernels hold the CUs their contributors need.
+static int nt_sk_mode() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_NT_SK");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+// units of 64 channels per 256x256 tile, and whether stream-K applies to this launch
+// GEMM dimensions for which stream-K runs (kg_bytes = B-row bytes: nu = kg_bytes / 128 K64 units).
+// conv_nt_group_rows returns 256 for these too, so the BN partial row groups match the 256-row
+// tiles whichever 256-row kernel ends up running (the stream-K kernel needs CA % 64 == 0 and no
+// halo staging; otherwise the plain 256x256 tile runs)
+static bool sk_dims(int M, int Nout, int kg_bytes) {
+  const int mode = nt_sk_mode();
+  if (mode == 0 || Nout < 128 || kg_bytes % 128 != 0) return false;
+  const int64_t tiles = (int64_t)((M + 255) / 256) * ((Nout + 255) / 256);
+  const int nu = kg_bytes / 128;
+  if (mode == 2) return nu >= 2;
+  return tiles < device_cus() && nu >= 8 && tiles * nu >= 2 * device_cus();
+}
+
+static bool use_stream_k(const NtArgs& a) {
+  // (a dgrad parity class may hold fewer taps than the B row: nu counts this launch's taps)
+  return a.CA % 64 == 0 && a.halo_rows == 0 && a.M > 0 && a.ntaps * (a.CA / 64) >= 2 &&
+         sk_dims(a.M, a.Nout, a.Kg * 2);
+}
+
+static std::atomic<int64_t> g_sk_launches{0};
+int64_t conv_stream_k_launches() { return g_sk_launches.load(); }
+
+template <int EPI>
+static void run_ntp_sk(const NtArgs& a, hipStream_t st) {
+  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
+  const int nu = a.ntaps * (a.CA / 64);
+  const int64_t total = (int64_t)ntm * ntn * nu;
+  const int cus = device_cus();
+  // per_wg <= nu: a range spans at most two tiles (the kernel runs two straight-line segments);
+  // nu / kSkMaxParts <= per_wg <= nu: at most kSkMaxParts partials per tile
+  const int per_wg = (int)std::max<int64_t>(std::min<int64_t>((total + cus - 1) / cus, nu),
+                                            (nu + kSkMaxParts - 1) / kSkMaxParts);
+  const int grid = (int)((total + per_wg - 1) / per_wg);
+  SkWorkspace* w = sk_workspace(st, cus);
+  if (w == nullptr) {  // first use under graph capture: no allocation possible
+    run_ntp<EPI, true>(a, st);
+    return;
+  }
+  auto kfn = igemm_ntp_kernel<EPI, true, true>;
+  constexpr int smem = 4 * 32768;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), smem, st, a,
+                     NtpSk{w->ws, w->flags, per_wg, (uint32_t)((size_t)cus * 65536 * sizeof(float))});
+  check_launch("igemm_ntp_sk");
+  g_sk_launches.fetch_add(1);
 }
 
 template <int WM, int WN, int TM, int TN, int EPI>
@@ -2167,6 +2600,7 @@ static bool use_mid_tile(int M, int Nout, int kg_bytes) {
 // size those buffers with it, dispatch_nt picks its tile with it -- one definition for both.
 int conv_nt_group_rows(int M, int Nout, int kg_bytes) {
   if (Nout <= 64) return 256;
+  if (sk_dims(M, Nout, kg_bytes)) return 256;  // stream-K (sub-wave grids of long-K 256x256 tiles)
   // small M takes the short 64x128 tile (enough blocks) -- unless the 256x256 grid alone fills the
   // chip: a 4096^3 GEMM (M = 4096) ran the 64x128 tile at 642 TF/s (VERDICT r3 weak #2 measured
   // that tile, not the 256x256 one)
@@ -2212,6 +2646,15 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     return;
   }
   if constexpr (C64 && OP == OP_BF16) {
+    if (use_stream_k(a)) {
+      run_ntp_sk<EPI>(a, st);
+      return;
+    }
+    if (rows == 256 && a.Nout > 64 && (ntq_mode() & 48)) {  // ping-pong wave groups
+      if (ntq_mode() & 32) run_ntp<EPI, true>(a, st);  // K64 stages
+      else run_ntp<EPI, false>(a, st);                 // K32 ring
+      return;
+    }
     if (rows == 256 && a.Nout > 64 && (ntq_mode() & 1)) {  // (Nout <= 64 is the 256x64 tile)
       if (ntq_mode() & 8) run_ntq<2, 4, 4, 2, EPI, OP_BF16, true>(a, st);
       else run_ntq<2, 4, 4, 2, EPI>(a, st);

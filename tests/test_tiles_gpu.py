@@ -440,3 +440,83 @@ def test_bn_reductions_concurrent_on_two_streams(gpu, native_ext):
     torch.cuda.synchronize()
     for o in outs:
         assert torch.equal(o, ref_stats)
+
+
+_SK_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+from pytorch_distributed_tutorials_amd import _C as C
+from pytorch_distributed_tutorials_amd.ops import reference as ref
+dev = torch.device("cuda:0")
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+out = {}
+# the sub-wave long-K shapes of ResNet-50 at batch 256: 196 / 196 / 98 tiles of 256x256
+for name, (n, h, w, c, k, r, s, st, pd) in {
+        "3x3_14": (256, 14, 14, 256, 256, 3, 3, 1, 1),
+        "1x1_14": (256, 14, 14, 1024, 256, 1, 1, 1, 0),
+        "3x3_7": (256, 7, 7, 512, 512, 3, 3, 1, 1)}.items():
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    wt = (torch.randn(k, c, r, s, generator=g) / (c * r * s) ** 0.5).to(torch.bfloat16).float().to(dev)
+    wt = wt.contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(dev)
+    M = n * h * w
+    before = C.conv_stream_k_launches()
+    y1, p1 = C.conv_fwd(x, C.pack_weight(wt, c), st, pd, True)
+    y2, p2 = C.conv_fwd(x, C.pack_weight(wt, c), st, pd, True)
+    dx1 = C.conv_dgrad(dy, wt, list(x.shape), st, pd)
+    dx2 = C.conv_dgrad(dy, wt, list(x.shape), st, pd)
+    # fresh operands between repeats: a partial read before its contributor stored it (or a
+    # stale cached copy) would carry the previous GEMM's values
+    xo = torch.randn(n, h, w, c, generator=g).to(torch.bfloat16).to(dev)
+    yo, _ = C.conv_fwd(xo, C.pack_weight(wt, c), st, pd, True)
+    y3, _ = C.conv_fwd(x, C.pack_weight(wt, c), st, pd, True)
+    torch.cuda.synchronize()
+    # compare repeats before bn_finalize (which may reduce the partials in place)
+    fwd_eq = bool(torch.equal(y1, y2) and torch.equal(p1, p2))
+    dgrad_eq = bool(torch.equal(dx1, dx2))
+    detail = {}
+    if not fwd_eq:
+        bad = ((y1.float() - y2.float()).abs() > 0).reshape(-1, k)
+        rows = bad.any(1).nonzero().flatten()
+        detail = {"y_equal": bool(torch.equal(y1, y2)), "p_equal": bool(torch.equal(p1, p2)),
+                  "bad_rows": rows.numel(), "row_tiles": sorted(set((rows // 256).tolist()))[:16],
+                  "col_tiles": sorted(set((bad.any(0).nonzero().flatten() // 256).tolist())),
+                  "p_rows_bad": ((p1 - p2).abs().reshape(p1.shape[0], -1) > 0).any(1).nonzero().flatten().tolist()[:16],
+                  "p_shape": list(p1.shape), "p_nan": bool(torch.isnan(p1).any() or torch.isnan(p2).any())}
+    yr = ref.conv2d_nhwc(x, wt, st, pd)
+    dxr = ref.conv2d_nhwc_dgrad(dy, wt, x.shape, st, pd)
+    stats = C.bn_finalize(p1, M, torch.zeros(k, device=dev), torch.ones(k, device=dev),
+                          torch.ones(k, device=dev), torch.zeros(k, device=dev), 0.1, 1e-5)
+    mean_r, var_r = ref.bn_batch_stats(yr)
+    out[name] = {"sk_launches": C.conv_stream_k_launches() - before,
+                 "fwd_rel": max(rel(y1, yr), rel(y3, yr)), "dgrad_rel": rel(dx1, dxr),
+                 "other_rel": rel(yo, ref.conv2d_nhwc(xo, wt, st, pd)),
+                 "mean_err": (stats[0] - mean_r).abs().max().item(),
+                 "invstd_rel": ((stats[1] - torch.rsqrt(var_r + 1e-5)).abs() / torch.rsqrt(var_r + 1e-5)).max().item(),
+                 "fwd_repeat_equal": fwd_eq, "dgrad_repeat_equal": dgrad_eq, "detail": detail}
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_stream_k_long_k_shapes_match_fp32(gpu, tmp_path, mode):
+    """Stream-K (PDT_NT_SK=1: sub-wave 256x256 grids; =2: forced wherever the kernel applies) on the
+    ResNet-50 long-K shapes: forward + BN partials and dgrad against fp32, and run-to-run bitwise
+    (partials are added in a fixed workgroup order)."""
+    env = dict(os.environ, PDT_NT_SK=mode)
+    r = subprocess.run([sys.executable, "-c", _SK_SCRIPT, ROOT], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    for name, v in res.items():
+        assert v["sk_launches"] >= 2, (name, v)  # the stream-K kernel ran (fwd twice at least)
+        assert v["fwd_rel"] < 1e-2 and v["dgrad_rel"] < 1e-2 and v["other_rel"] < 1e-2, (name, v)
+        assert v["mean_err"] < 2e-3 and v["invstd_rel"] < 2e-2, (name, v)
+        assert v["fwd_repeat_equal"] and v["dgrad_repeat_equal"], (name, v)
