@@ -257,12 +257,33 @@ def main(argv=None) -> int:
     # host issue cost of one step from an idle device (untimed, after the timed region): the time
     # inside step() above also counts waits on a full launch queue whenever the GPU is the bound
     issue = []
+    prof_path = os.environ.get("PDT_HOST_PROFILE")  # cProfile of these idle-device steps (diagnostic)
+    prof = None
+    if prof_path and env.rank == 0:
+        import cProfile
+        prof = cProfile.Profile()
     for _ in range(3):
         barrier()
         th = time.perf_counter()
-        step()
+        if prof is not None:
+            # backward on this thread, so cProfile sees the autograd Functions' Python too
+            with torch.autograd.set_multithreading_enabled(False):
+                prof.enable()
+                step()
+                prof.disable()
+        else:
+            step()
         issue.append(time.perf_counter() - th)
     barrier()
+    if prof is not None:
+        import io
+        import pstats
+        buf = io.StringIO()
+        st_ = pstats.Stats(prof, stream=buf)
+        st_.sort_stats("tottime").print_stats(60)
+        st_.sort_stats("cumulative").print_stats(60)
+        with open(prof_path, "w") as f:
+            f.write(buf.getvalue())
     host_issue_ms = 1000.0 * min(issue)
     comm = None
     if args.impl == "native":

@@ -81,5 +81,10 @@ def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
     # both learn (the loss falls well below its start), and track each other window by window
     assert n[-1] < 0.2 * n[0] and s[-1] < 0.2 * s[0], (n, s)
     assert res["native_train_acc"] > 0.9 and res["stock_train_acc"] > 0.9, res
+    # fp8 band: the steepest part of the curve (windows 4-6) is where e4m3 activations / e5m2
+    # gradients shift the descent by a few steps; two r4 runs of the same config (the fp8 weight
+    # gradients accumulate with atomics: not bitwise reproducible) differed by 0.23 in window 5
+    # (native 1.71 / 1.48 vs stock 1.25).  bf16 keeps the ResNet-18 band.
+    a_tol, r_tol = (0.25, 0.35) if fp8 else (0.15, 0.25)
     for a, b in zip(n, s):
-        assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)
+        assert abs(a - b) <= a_tol + r_tol * b, (n, s)
