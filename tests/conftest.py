@@ -31,6 +31,24 @@ def gpu(native_ext):
     return torch.device("cuda:0")
 
 
+def parse_results(text: str) -> list:
+    """Every JSON object printed after a "RESULT " marker.  Ranks of a multi-process test print
+    through one pipe and their lines can interleave (two payloads on one line), so each payload is
+    decoded with raw_decode from its marker instead of assuming one object per line."""
+    import json
+    dec, res, pos = json.JSONDecoder(), [], 0
+    while True:
+        pos = text.find("RESULT ", pos)
+        if pos < 0:
+            return res
+        try:
+            obj, end = dec.raw_decode(text, pos + len("RESULT "))
+            res.append(obj)
+            pos = end
+        except json.JSONDecodeError:
+            pos += len("RESULT ")
+
+
 def free_port() -> int:
     """A TCP port on 127.0.0.1 that is free right now (for launcher rendezvous in tests)."""
     import socket

@@ -19,7 +19,7 @@ import sys
 import time
 
 import pytest
-from conftest import free_port
+from conftest import free_port, parse_results
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -36,19 +36,7 @@ def _run(fault=None, timeout=5.0, nproc=2):
            "--timeout", str(timeout)]
     t0 = time.time()
     r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=240, capture_output=True, text=True)
-    # both ranks print through one pipe: under load their lines can interleave, so decode every
-    # "RESULT " payload with raw_decode instead of assuming one JSON object per line
-    dec, res, pos = json.JSONDecoder(), [], 0
-    while True:
-        pos = r.stdout.find("RESULT ", pos)
-        if pos < 0:
-            break
-        try:
-            obj, end = dec.raw_decode(r.stdout, pos + len("RESULT "))
-            res.append(obj)
-            pos = end
-        except json.JSONDecodeError:
-            pos += len("RESULT ")
+    res = parse_results(r.stdout)  # interleaved rank output: see conftest.parse_results
     return r, {x["rank"]: x for x in res}, time.time() - t0
 
 

@@ -24,6 +24,7 @@ import sys
 import pytest
 import torch
 import torch.nn.functional as F
+from conftest import parse_results
 
 from pytorch_distributed_tutorials_amd.ops import reference as ref
 
@@ -513,8 +514,7 @@ def test_stream_k_long_k_shapes_match_fp32(gpu, tmp_path, mode):
     r = subprocess.run([sys.executable, "-c", _SK_SCRIPT, ROOT], env=env, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1]
-    res = json.loads(line[len("RESULT "):])
+    res = parse_results(r.stdout)[-1]
     for name, v in res.items():
         assert v["sk_launches"] >= 2, (name, v)  # the stream-K kernel ran (fwd twice at least)
         assert v["fwd_rel"] < 1e-2 and v["dgrad_rel"] < 1e-2 and v["other_rel"] < 1e-2, (name, v)

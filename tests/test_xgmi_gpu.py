@@ -21,7 +21,7 @@ import sys
 
 import pytest
 import torch
-from conftest import free_port
+from conftest import free_port, parse_results
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
@@ -167,7 +167,7 @@ def _launch(mode, nproc):
     cmd = [sys.executable, "-m", "pytorch_distributed_tutorials_amd.launch", f"--nproc_per_node={nproc}",
            "--master_port", str(free_port()), os.path.join(ROOT, "tests", "xgmi_worker.py"), "--mode", mode]
     r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=200, capture_output=True, text=True)
-    res = [json.loads(l[7:]) for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+    res = parse_results(r.stdout)
     return r, {x["rank"]: x for x in res}
 
 
