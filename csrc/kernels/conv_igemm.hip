@@ -1708,6 +1708,7 @@ struct TnArgs {
   int staged;          // epilogue through the LDS row image (256-B segments); 0 = direct (A/B knob)
   int Ho;
   int adv_r, adv_qh, adv_qn;  // 64 rows = (adv_qn images, adv_qh output rows, adv_r columns)
+  int nblocks;                // > 0: grid-capped launch looping over this many logical blocks
 };
 
 // LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
@@ -1800,17 +1801,15 @@ constexpr int tn_threads() { return BMG == 256 ? 512 : 256; }  // == TnCfg<BMG, 
 // PW: pointwise conv (1x1, stride 1, no padding): the x row of reduction index m IS pixel m, so a
 // B offset is m*C*2 + channel bytes -- no pixel decomposition, no bounds test (rows past the end
 // fall outside the buffer and read 0).
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING = false>
-__global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING>
+__device__ __forceinline__ void tn_block(const TnArgs& P, int vb, int nblocks, char* smem) {
   using CFG = TnCfg<BMG, BNG, STAGES, RING>;
-  static_assert(CFG::NT == tn_threads<BMG>(), "launch bounds");
   constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int ntn = (P.Ncols + BNG - 1) / BNG;
   const int ntm = (P.Kout + BMG - 1) / BMG;
   const int tiles = ntm * ntn;
-  const int lid = xcd_remap(blockIdx.x, (int)gridDim.x);
+  const int lid = xcd_remap(vb, nblocks);
   const int split = lid / tiles;
   const int bid = lid - split * tiles;
   const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
@@ -2054,6 +2053,25 @@ __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArg
         }
       }
     }
+}
+
+// Grid-capped launch (TnArgs::nblocks > 0, PDT_TN_GRID_CAP): gridDim.x workgroups loop over the
+// nblocks logical blocks, so the weight-gradient stream never holds more than the cap's share of
+// the CUs while the dgrad chain runs beside it.  Measured (r4u, ResNet-50 b256): no cap 19.06 ms,
+// cap 256 19.37, 512 19.07, 768 19.06; --force-comm 19.60 with and without cap 512 -- it does not
+// replace the main-stream priority, so it stays an A/B knob (profiles/r4u_tn_grid_cap_ab.jsonl).
+template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING = false>
+__global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
+  static_assert(TnCfg<BMG, BNG, STAGES, RING>::NT == tn_threads<BMG>(), "launch bounds");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (P.nblocks <= 0) {
+    tn_block<BMG, BNG, STAGES, ATOMIC, PW, RING>(P, blockIdx.x, gridDim.x, smem);
+    return;
+  }
+  for (int vb = blockIdx.x; vb < P.nblocks; vb += gridDim.x) {
+    tn_block<BMG, BNG, STAGES, ATOMIC, PW, RING>(P, vb, P.nblocks, smem);
+    __syncthreads();  // the epilogue's LDS staging is read before the next block's DMA lands
+  }
 }
 
 // ============================================================================
@@ -2938,7 +2956,20 @@ static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kfn, dim3(tiles * splits), dim3(CFG::NT), CFG::SMEM, st, a);
+  // PDT_TN_GRID_CAP=<n>: at most n workgroups, looping over the tiles x splits blocks (A/B knob)
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("PDT_TN_GRID_CAP");
+    cap = e ? std::max(0, atoi(e)) : 0;
+  }
+  const int nb = tiles * splits;
+  if (cap > 0 && nb > cap) {
+    TnArgs b = a;
+    b.nblocks = nb;
+    hipLaunchKernelGGL(kfn, dim3(cap), dim3(CFG::NT), CFG::SMEM, st, b);
+  } else {
+    hipLaunchKernelGGL(kfn, dim3(nb), dim3(CFG::NT), CFG::SMEM, st, a);
+  }
   check_launch("igemm_tn");
 }
 
