@@ -2335,12 +2335,15 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
 // PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
 // tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile, bit 4 / bit 5 = the
-// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 33 = ping-pong K64; 1 = the quadrant-phased kernel; 0 = none)
+// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 1 = the quadrant-phased kernel; 33 = ping-pong K64; 0 = none)
 static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PDT_NTQ");
-    v = e ? atoi(e) : 33;  // ping-pong K64 256x256 (r4h: 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899)
+    // default 1 (quadrant-phased).  The ping-pong K64 kernel (33) wins the isolated GEMMs (r4h:
+    // 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899) but loses ~0.1 ms in the ResNet-50 step
+    // (r4h 18.94 vs 18.81 ms, r4z 19.19 vs 19.11 ms)
+    v = e ? atoi(e) : 1;
   }
   return v;
 }
