@@ -2335,15 +2335,16 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
 // C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
 // PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
 // tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile, bit 4 / bit 5 = the
-// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 1 = the quadrant-phased kernel; 33 = ping-pong K64; 0 = none)
+// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 3 = the quadrant-phased kernel on both; 33 = ping-pong K64; 0 = none)
 static int ntq_mode() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PDT_NTQ");
-    // default 1 (quadrant-phased).  The ping-pong K64 kernel (33) wins the isolated GEMMs (r4h:
-    // 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899) but loses ~0.1 ms in the ResNet-50 step
-    // (r4h 18.94 vs 18.81 ms, r4z 19.19 vs 19.11 ms)
-    v = e ? atoi(e) : 1;
+    // default 3: the quadrant-phased kernel on the 256x256 AND the 128x128 bf16 tiles (r4ab,
+    // interleaved: 18.86 / 18.85 ms vs 18.93 / 18.92 / 18.97 with 1).  The ping-pong K64 kernel
+    // (33) wins the isolated GEMMs (r4h: 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899) but loses
+    // ~0.1 ms in the ResNet-50 step (r4h 18.94 vs 18.81 ms, r4z 19.19 vs 19.11 ms)
+    v = e ? atoi(e) : 3;
   }
   return v;
 }

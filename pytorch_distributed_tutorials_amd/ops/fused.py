@@ -42,13 +42,13 @@ _FP8_WGRAD = os.environ.get("PDT_FP8_WGRAD", "1") != "0"
 # fp8-only storage: activations / input gradients whose every consumer reads the fp8 copy are not
 # written in bf16 at all (interior bottleneck outputs, and dy of convs with fp8 dgrad + fp8 wgrad)
 _FP8_ONLY = os.environ.get("PDT_FP8_ONLY", "1") != "0"
-# PDT_BN_ACC=1 (A/B knob, non-deterministic runs only): BN-backward sums of a BN-fused dgrad
-# accumulated by its epilogue's fp32 atomics into a per-BN [2, C] buffer -- no partial buffer and
-# no reduce launch on the main stream; the consuming apply adds the BN parameter gradients, and the
-# buffer is re-zeroed on the weight-gradient side stream once the apply is done.  Measured neutral
-# (r3t, one box: 18.949 / 18.944 ms off vs 18.925 / 18.983 on): the 47 reduce launches it removes
-# sat beside weight-gradient work that filled the GPU, so off (deterministic sums) by default.
-_BN_ACC = os.environ.get("PDT_BN_ACC", "0") == "1"
+# PDT_BN_ACC (non-deterministic runs only; deterministic runs always take the partial buffers):
+# BN-backward sums of a BN-fused dgrad accumulated by its epilogue's fp32 atomics into a per-BN
+# [2, C] buffer -- no partial buffer and no reduce launch on the main stream; the consuming apply
+# adds the BN parameter gradients, and the buffer is re-zeroed on the weight-gradient side stream
+# once the apply is done.  Round 3 measured it neutral (r3t); with round 4's kernels it pays
+# (r4ab, interleaved, with PDT_NTQ=3: 18.78 / 18.72 ms on vs 18.86 / 18.85 off), so on by default.
+_BN_ACC = os.environ.get("PDT_BN_ACC", "1") == "1"
 
 
 def _bacc(p, c):
