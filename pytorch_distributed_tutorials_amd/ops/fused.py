@@ -784,6 +784,11 @@ def _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, moment
     count = n * ((h + 2 * pad - r) // stride + 1) * ((wd + 2 * pad - s) // stride + 1)
     if x8 is not None and not _fp8_conv_ok(r, s, cx) and x is not None:
         x8 = None  # a GEMM K of 64 (1x1 over 64 channels) half-fills the 128-wide fp8 K-step: bf16 is faster
+    if x8 is None and training and not _NAN_TRACE:
+        # conv + BN finalize in one host call (the running-stat update waits for the buffers first)
+        buffers_ready()
+        return C.conv_fwd_bn(x, _packed_krsc(C, w, cx), stride, pad, count, rm, rv, gamma, beta,
+                             float(momentum), float(eps))
     if x8 is not None:
         wq, wsc = _packed_krsc8(C, w, cx)
         y, part = C.conv_fwd_fp8(x8[0], wq, wsc, stride, pad, training, x8[1])
