@@ -355,8 +355,19 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fp8(const Tensor& dy8, const Tensor& wt
 }
 
 // dw as an fp32 channels_last tensor of logical shape [K, C, R, S]
+static Tensor conv_wgrad_impl(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
+                              int64_t pad, bool deterministic, const std::optional<Tensor>& out,
+                              float* zero, int zero_n);
+
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
                   int64_t pad, bool deterministic, const std::optional<Tensor>& out) {
+  return conv_wgrad_impl(dy, x, ws, stride, pad, deterministic, out, nullptr, 0);
+}
+
+// zero / zero_n: a buffer the weight-gradient kernel clears (see launch_conv_wgrad)
+static Tensor conv_wgrad_impl(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, int64_t stride,
+                              int64_t pad, bool deterministic, const std::optional<Tensor>& out,
+                              float* zero, int zero_n) {
   check_bf16_nhwc(dy, "dy");
   check_bf16_nhwc(x, "x");
   TORCH_CHECK(ws.size() == 4, "weight shape must be [K,C,R,S]");
@@ -380,12 +391,12 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, std::vector<int64_t> ws, in
     for (int d = 0; d < 4; ++d)
       TORCH_CHECK(o.size(d) == 1 || o.stride(d) == want[d], "wgrad out must be channels_last (KRSC) dense");
     pdt::launch_conv_wgrad(cbf(dy), cbf(x), o.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
-                           s, deterministic, true, cur_stream(x));
+                           s, deterministic, true, cur_stream(x), zero, zero_n);
     return o;
   }
   auto dwp = at::empty({K, R, S, Cx}, fopt);
   pdt::launch_conv_wgrad(cbf(dy), cbf(x), dwp.data_ptr<float>(), wsn ? wsb.data_ptr<float>() : nullptr,
-                         s, deterministic, false, cur_stream(x));
+                         s, deterministic, false, cur_stream(x), zero, zero_n);
   Tensor krsc = Cx == C ? dwp : dwp.narrow(3, 0, C).contiguous();
   return krsc.permute({0, 3, 1, 2});  // [K,C,R,S] view with channels_last strides
 }
@@ -415,11 +426,17 @@ Tensor conv_wgrad_side(int64_t side, const Tensor& dy, const Tensor& x, std::vec
   Tensor r;
   {
     c10::hip::HIPStreamGuard sg(sst);
-    r = conv_wgrad(dy, x, ws, stride, pad, deterministic, out);
     // `zero`: a BN-sum accumulator whose consumer (the apply just queued on the current stream) is
-    // done at this point of the side stream: re-zeroed here, off the critical path, for its next use
-    if (zero.has_value() && zero->defined())
-      TORCH_CHECK(hipMemsetAsync(zero->data_ptr(), 0, zero->nbytes(), sst.stream()) == hipSuccess, "memset");
+    // done at this point of the side stream: the weight-gradient kernel itself re-zeroes it for its
+    // next use (workgroup 0), off the critical path and without a memset launch
+    float* zp = nullptr;
+    int zn = 0;
+    if (zero.has_value() && zero->defined()) {
+      TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous(), "zero: contiguous fp32");
+      zp = zero->data_ptr<float>();
+      zn = (int)zero->numel();
+    }
+    r = conv_wgrad_impl(dy, x, ws, stride, pad, deterministic, out, zp, zn);
   }
   c10::hip::HIPCachingAllocator::recordStream(dy.storage().data_ptr(), sst);
   c10::hip::HIPCachingAllocator::recordStream(x.storage().data_ptr(), sst);

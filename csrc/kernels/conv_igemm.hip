@@ -1709,6 +1709,8 @@ struct TnArgs {
   int Ho;
   int adv_r, adv_qh, adv_qn;  // 64 rows = (adv_qn images, adv_qh output rows, adv_r columns)
   int nblocks;                // > 0: grid-capped launch looping over this many logical blocks
+  float* zero;                // optional: zero_n floats workgroup 0 clears (a consumed BN-sum
+  int zero_n;                 //   accumulator, re-zeroed without a memset launch)
 };
 
 // LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
@@ -2064,6 +2066,8 @@ template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING = false>
 __global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
   static_assert(TnCfg<BMG, BNG, STAGES, RING>::NT == tn_threads<BMG>(), "launch bounds");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (P.zero != nullptr && blockIdx.x == 0)  // ordered after the accumulator's consumer by the caller
+    for (int i = threadIdx.x; i < P.zero_n; i += blockDim.x) P.zero[i] = 0.f;
   if (P.nblocks <= 0) {
     tn_block<BMG, BNG, STAGES, ATOMIC, PW, RING>(P, blockIdx.x, gridDim.x, smem);
     return;
@@ -3037,7 +3041,8 @@ void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* d
 }
 
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st) {
+                       const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
+                       float* zero, int zero_n) {
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
   WgradPlan p = plan_wgrad(s, deterministic);
   const bool slab = deterministic && p.splits > 1;
@@ -3055,6 +3060,8 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
   a.steps_per_split = p.steps_per_split;
   a.nsteps = p.nsteps;
   a.accumulate = (accumulate && !slab) ? 1 : 0;  // slabs are private partials: always overwritten
+  a.zero = zero_n > 0 ? zero : nullptr;
+  a.zero_n = zero_n;
   static int staged = -1;
   if (staged < 0) {
     const char* e = getenv("PDT_TN_STAGED");
