@@ -520,3 +520,21 @@ def test_stream_k_long_k_shapes_match_fp32(gpu, tmp_path, mode):
         assert v["fwd_rel"] < 1e-2 and v["dgrad_rel"] < 1e-2 and v["other_rel"] < 1e-2, (name, v)
         assert v["mean_err"] < 2e-3 and v["invstd_rel"] < 2e-2, (name, v)
         assert v["fwd_repeat_equal"] and v["dgrad_repeat_equal"], (name, v)
+
+
+@pytest.mark.parametrize("ntq", ["0", "17", "33"])
+def test_wide_tile_main_loops_match_fp32(gpu, tmp_path, ntq):
+    """The opt-in 256x256 main loops (PDT_NTQ: 0 = round-3 2-stage loop, 17 = ping-pong K32 ring,
+    33 = ping-pong K64) on the long-K shapes that take the wide tile: forward + BN partials and
+    dgrad against fp32, run-to-run bitwise (the default quadrant-phased loop is what every other
+    tile test runs)."""
+    env = dict(os.environ, PDT_NTQ=ntq, PDT_NT_SK="0")
+    r = subprocess.run([sys.executable, "-c", _SK_SCRIPT, ROOT], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = parse_results(r.stdout)[-1]
+    for name, v in res.items():
+        assert v["sk_launches"] == 0, (name, v)
+        assert v["fwd_rel"] < 1e-2 and v["dgrad_rel"] < 1e-2 and v["other_rel"] < 1e-2, (name, v)
+        assert v["mean_err"] < 2e-3 and v["invstd_rel"] < 2e-2, (name, v)
+        assert v["fwd_repeat_equal"] and v["dgrad_repeat_equal"], (name, v)
