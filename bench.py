@@ -57,6 +57,9 @@ def parse(argv=None):
     p.add_argument("--force-comm", action="store_true",
                    help="native impl: run the RCCL communicator + C++ reducer + buffer broadcasts "
                         "even at N=1 (world-1 RCCL communicator; exercises the multi-GPU path)")
+    p.add_argument("--plan-world", type=int, default=None,
+                   help="world size the bucket layout is planned for (default: the job's; with "
+                        "--force-comm at N=1: 8, so one GPU runs the 8-rank layout incl. its tail bucket)")
     p.add_argument("--no-broadcast-buffers", action="store_true",
                    help="DDP broadcast_buffers=False: BatchNorm running stats stay per-rank")
     p.add_argument("--comm-timing", action="store_true",
@@ -98,6 +101,34 @@ def _relaunch_with_torchrun(args_argv, n) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+def _param_checksums(ddp, impl, world, dev):
+    """(all ranks identical?, rank 0's checksum): sum_i bits(p_i) * (i % 8191 + 1) in int64 over
+    every parameter in order, gathered from every rank."""
+    import torch
+    import torch.distributed as dist
+    with torch.no_grad():
+        if impl == "native":
+            flats = [ddp.space.param_flat]
+        else:
+            flats = [p.detach().reshape(-1) for p in ddp.parameters()]
+        total = torch.zeros((), dtype=torch.int64, device=dev)
+        base = 0
+        for f in flats:
+            bits = f.contiguous().view(torch.int32).to(torch.int64)
+            idx = torch.arange(base, base + bits.numel(), device=bits.device, dtype=torch.int64)
+            total += (bits * (idx % 8191 + 1)).sum().to(dev)
+            base += bits.numel()
+    if world > 1:
+        if dist.get_backend() == "gloo":
+            total = total.cpu()
+        out = [torch.zeros_like(total) for _ in range(world)]
+        dist.all_gather(out, total)
+        vals = [int(v.item()) for v in out]
+    else:
+        vals = [int(total.item())]
+    return all(v == vals[0] for v in vals), vals[0]
 
 
 def _last_mb(v: str):
@@ -167,7 +198,8 @@ def main(argv=None) -> int:
                                       first_bucket_mb=args.first_bucket_mb,
                                       last_bucket_mb=args.last_bucket_mb,
                                       force_reducer=args.force_comm, comm_options=copts, comm=args.comm,
-                                      broadcast_buffers=not args.no_broadcast_buffers)
+                                      broadcast_buffers=not args.no_broadcast_buffers,
+                                      plan_world=args.plan_world or (8 if args.force_comm and world == 1 else None))
         holder["ddp"] = ddp
         if args.comm_timing:
             ddp.enable_comm_timing(True)
@@ -285,6 +317,9 @@ def main(argv=None) -> int:
         with open(prof_path, "w") as f:
             f.write(buf.getvalue())
     host_issue_ms = 1000.0 * min(issue)
+    # every rank must hold bit-identical parameters after the run (untimed): a positional int64
+    # checksum of the parameter bits, all-gathered -- a fast-but-wrong multi-GPU run shows here
+    ranks_identical, param_checksum = _param_checksums(ddp, args.impl, world, dev)
     comm = None
     if args.impl == "native":
         info = ddp.bucket_info()
@@ -337,7 +372,9 @@ def main(argv=None) -> int:
                        "deterministic": bool(args.deterministic), "force_comm": bool(args.force_comm),
                        "first_bucket_mb": args.first_bucket_mb,
                        "last_bucket_mb": ddp.last_bucket_mb if args.impl == "native" else args.last_bucket_mb,
-                       "comm": comm, "final_loss": round(final_loss, 4)},
+                       "plan_world": getattr(ddp, "plan_world", world) if args.impl == "native" else world,
+                       "comm": comm, "final_loss": round(final_loss, 4),
+                       "ranks_identical": ranks_identical, "param_checksum": param_checksum},
         }
         line = json.dumps(res)
         print(line, flush=True)

@@ -1518,6 +1518,7 @@ PYBIND11_MODULE(_C, m) {
       .def("open_peers", &pdt::XgmiComm::open_peers, py::arg("handles"))
       .def("link_local", &pdt::XgmiComm::link_local, py::arg("comms"))
       .def("grad_buffer", &pdt::XgmiComm::grad_buffer)
+      .def_property_readonly("flags_uncached", &pdt::XgmiComm::flags_uncached)
       .def("reduce_bucket", &pdt::XgmiComm::reduce_bucket, py::arg("bucket"), py::arg("offset"),
            py::arg("count"), py::arg("average") = true)
       .def("reduce_bucket_phases", &pdt::XgmiComm::reduce_bucket_phases, py::arg("bucket"), py::arg("offset"),

@@ -32,7 +32,28 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t numel, int nbuckets,
   hipc(hipMalloc(&g_, numel * sizeof(float)), "hipMalloc(grad)");
   hipc(hipMalloc(&red_, numel * sizeof(float)), "hipMalloc(reduced)");
   const size_t fbytes = (size_t)nbuckets * 2 * 8 * sizeof(unsigned);
-  hipc(hipMalloc(&flags_, fbytes), "hipMalloc(flags)");
+  // The per-bucket epoch flags are stored into by PEER GPUs and spin-polled here: keep them in
+  // uncached (fine-grained) device memory, as RCCL does for its cross-GPU flags and FIFOs, so a
+  // poll never hits a stale line of the local L2 whatever the coherence of peer stores through
+  // xGMI.  Fall back to plain memory only if the runtime cannot export the allocation.
+  flags_uncached_ = false;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), fbytes, hipDeviceMallocUncached) == hipSuccess) {
+    hipIpcMemHandle_t probe;
+    if (hipIpcGetMemHandle(&probe, flags_) == hipSuccess) {
+      flags_uncached_ = true;
+    } else {
+      (void)hipGetLastError();
+      hipFree(flags_);
+      flags_ = nullptr;
+    }
+  } else {
+    (void)hipGetLastError();
+    flags_ = nullptr;
+  }
+  if (!flags_uncached_) {
+    fprintf(stderr, "[xgmi] uncached flag memory not exportable here; using plain device memory\n");
+    hipc(hipMalloc(&flags_, fbytes), "hipMalloc(flags)");
+  }
   hipc(hipMemset(g_, 0, numel * sizeof(float)), "hipMemset");
   if (wire == "bf16") {
     hipc(hipMalloc(&g16_, numel * sizeof(uint16_t)), "hipMalloc(grad bf16)");

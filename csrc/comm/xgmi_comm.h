@@ -33,6 +33,7 @@ class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
   hipStream_t stream() const { return stream_.stream(); }
 
   bool wire_bf16() const { return g16_ != nullptr; }
+  bool flags_uncached() const { return flags_uncached_; }
   int max_blocks() const { return max_blocks_; }
   // IPC handles of (gradient buffer, reduced-shard buffer, flag array[, bf16 gradient copy,
   // bf16 reduced shards]), concatenated
@@ -71,6 +72,7 @@ class XgmiComm : public std::enable_shared_from_this<XgmiComm> {
   float* g_ = nullptr;
   float* red_ = nullptr;
   unsigned* flags_ = nullptr;
+  bool flags_uncached_ = false;  // flags in hipDeviceMallocUncached memory (fine-grained)
   uint16_t* g16_ = nullptr;   // bf16 wire only
   uint16_t* red16_ = nullptr;
   int max_blocks_ = 16;

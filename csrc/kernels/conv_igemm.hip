@@ -30,6 +30,7 @@
 // one barrier per K-step.  Block ids are remapped so consecutive tiles (sharing
 // the A panel) run on the same XCD and hit its L2.
 #include "common.h"
+#include "igemm_common.h"
 #include "kernels.h"
 
 #include <algorithm>
@@ -45,43 +46,6 @@
 
 namespace pdt {
 
-typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-
-// ---------------------------------------------------------------- utilities
-struct FastDiv {  // n / d for 0 <= n < 2^31 via mul-hi
-  uint32_t mul, shr;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  f.shr = l;
-  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  uint32_t hi = __umulhi(n, f.mul);
-  return (hi + n) >> f.shr;
-}
-
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  // bijective: blocks b, b+8, b+16, ... (one XCD under round-robin dispatch) get consecutive ids
-  int q = nwg / 8, r = nwg % 8;
-  int xcd = bid % 8, loc = bid / 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-}
-
-__device__ __forceinline__ v4i buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-__device__ __forceinline__ v4f mfma16(const v4i& a, const v4i& b, const v4f& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a),
-                                                __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
-}
-
-constexpr uint32_t OOB = 0x80000000u;  // any offset >= num_records reads 0
 
 // Operand element type of the NT kernel: bf16, or fp8 with the activation operand in e4m3
 // (forward) or e5m2 (gradients); weights are always e4m3.  A K-step moves 128 bytes of every
@@ -254,36 +218,6 @@ struct NtCfg {
   static constexpr int SMEM = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
 };
 
-// 16-byte LDS-DMA: every lane fetches 16 B at its own buffer offset (out-of-range -> 0) and the
-// wave's 64 results land contiguously at `lds` (wave-uniform base, lane-linear image).
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      r, (__attribute__((address_space(3))) void*)(reinterpret_cast<uintptr_t>(lds)), 16, voff, 0, 0, 0);
-}
-
-// Wait until at most N of this wave's vector-memory ops (LDS-DMA included) are outstanding.
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// Workgroup barrier WITHOUT the memory-model fence of __syncthreads(): that fence makes the compiler
-// emit s_waitcnt vmcnt(0) before s_barrier, draining every in-flight LDS-DMA and defeating a
-// multi-stage pipeline.  Callers order memory themselves: their own counted vmcnt wait covers the
-// DMA into the buffer about to be read, and every ds_read of the buffer about to be refilled has
-// been consumed (lgkmcnt 0) by the MFMAs before the barrier.  The "memory" clobber keeps the
-// compiler from moving LDS accesses across it.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-// Multi-stage pipelines: every K-step issues LPS DMA ops per wave; wait until the oldest pending
-// step has landed while `younger` later steps (wave-uniform, < 5) may stay in flight.
-template <int LPS>
-__device__ __forceinline__ void wait_steps(int younger) {
-  if (younger >= 4) wait_vm<4 * LPS>();
-  else if (younger == 3) wait_vm<3 * LPS>();
-  else if (younger == 2) wait_vm<2 * LPS>();
-  else if (younger == 1) wait_vm<LPS>();
-  else wait_vm<0>();
-}
 
 // Main loop: LDS-DMA staging (no VGPR round trip, no ds_write), the XOR swizzle applied on the
 // SOURCE side (lane slot j of row r fetches chunk j ^ f(r)) so the lane-linear LDS image equals
@@ -1134,12 +1068,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
 // Rows are permuted so that each wave's 4 quadrant sub-tiles form ONE contiguous 128x64 output
 // tile (8 waves = 2 (M) x 4 (N)): X half hx holds GEMM rows {wm*128 + hx*64 + [0,64)}, W half
 // hw holds channels {wn*64 + hw*32 + [0,32)}, so nt_epilogue runs unchanged (WM 2, WN 4,
-// TM 8, TN 4).  C64 (per-tap 64-channel K-steps) loader only.
-// barrier that also retires this wave's own LDS reads first: the quarter refilled right after it
-// must not have a fragment read of any wave still in flight (the MFMAs that consume the reads
-// are not memory operations, so the compiler may place them -- and their lgkmcnt wait -- after
-// an asm barrier)
-__device__ __forceinline__ void lds_barrier_rd() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Geometry: WM x WN waves, each owning a contiguous (2*TMQ*16) x (2*TNQ*16) output tile made of
 // its four quadrant sub-tiles (TMQ x TNQ MFMA tiles each).  256x256: 8 waves (2 x 4), TMQ 4,
@@ -1713,50 +1641,6 @@ struct TnArgs {
   int zero_n;                 //   accumulator, re-zeroed without a memset launch)
 };
 
-// LDS image of a [64 m][128 col] bf16 tile: 256-B rows, 16-B chunks XOR-swizzled by
-// swz(m)<<1 with swz(m) = (m&3) | ((m>>3)&1)<<2.  The transposing fragment read
-// (ds_read_b64_tr_b16: per 32-lane half, rows {m..m+3, m+8..m+11} x 32 B) then hits
-// 8 distinct 32-B bank windows: conflict-free; ds_write_b128 groups stay in one half-row.
-__device__ __forceinline__ int swz256(int row, int chunk) {
-  int sw = (row & 3) | (((row >> 3) & 1) << 2);
-  return row * 256 + ((chunk ^ (sw << 1)) << 4);
-}
-
-typedef short v4s_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ v4s_t ds_read_tr(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s_t*)(reinterpret_cast<uintptr_t>(p)));
-}
-
-__device__ __forceinline__ v4i cat_frag(v4s_t lo, v4s_t hi) {
-  return __builtin_bit_cast(v4i, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// 128-B-row variant for the [64 m][64 kout] A tile of a BMG = 64 wgrad: swizzle
-// sw(m) = ((m>>1)&1) | ((m>>3)&1)<<1 applied as chunk ^ (sw<<1) keeps each tr-read chunk pair
-// together; a half-wave's rows {m..m+3, m+8..m+11} land in 8 distinct 32-B bank windows
-// ((m&1)*4 + (pair ^ sw)), so the 128-B image is conflict-free too and the tile DMA moves only
-// the bytes the MFMAs consume (the 256-B image fetched a never-read upper half).
-__device__ __forceinline__ int swz128_tr(int row, int chunk) {
-  int sw = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-  return row * 128 + ((chunk ^ (sw << 1)) << 4);
-}
-
-// 512-B rows (the [64 m][256 kout] dy tile of a BMG = 256 wgrad): the swz256 XOR on chunk bits
-// 1..3 -- LDS banks repeat every 256 B, so a half-wave's rows {m..m+3, m+8..m+11} still land in 8
-// distinct 32-B bank windows.
-__device__ __forceinline__ int swz512(int row, int chunk) {
-  int sw = (row & 3) | (((row >> 3) & 1) << 2);
-  return row * 512 + ((chunk ^ (sw << 1)) << 4);
-}
-
-template <int ROWB>
-__device__ __forceinline__ int swz_img(int row, int chunk) {
-  if constexpr (ROWB == 512) return swz512(row, chunk);
-  else if constexpr (ROWB == 256) return swz256(row, chunk);
-  else return swz128_tr(row, chunk);
-}
 
 // RING: the stages are K32 slots (32 reduction rows of both operands) in a ring of STAGES = 4,
 // refilled three slots (1.5 K64 steps) ahead with counted vmcnt waits and one barrier per slot,
@@ -2945,12 +2829,25 @@ static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
   return p;
 }
 
+void conv_wgrad_plan_v2(const ConvShape& s, bool deterministic, int out[4]);
+size_t conv_wgrad_ws_floats_v2(const ConvShape& s, bool deterministic);
+void launch_conv_wgrad_v2(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
+                          const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
+                          float* zero, int zero_n);
+static bool wg_v1() {  // PDT_WG_V1=1: the round-4 TN kernel (A/B only)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("PDT_WG_V1"); v = (e && e[0] == '1') ? 1 : 0; }
+  return v == 1;
+}
+
 void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]) {
+  if (!wg_v1()) return conv_wgrad_plan_v2(s, deterministic, out);
   const WgradPlan p = plan_wgrad(s, deterministic);
   out[0] = p.bmg; out[1] = p.bng; out[2] = p.tiles; out[3] = p.splits;
 }
 
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
+  if (!wg_v1()) return conv_wgrad_ws_floats_v2(s, deterministic);
   if (!deterministic) return 0;
   WgradPlan p = plan_wgrad(s, true);
   if (p.splits <= 1) return 0;
@@ -3043,6 +2940,7 @@ void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* d
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
                        const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
                        float* zero, int zero_n) {
+  if (!wg_v1()) return launch_conv_wgrad_v2(dy, x, dw, ws, s, deterministic, accumulate, st, zero, zero_n);
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
   WgradPlan p = plan_wgrad(s, deterministic);
   const bool slab = deterministic && p.splits > 1;

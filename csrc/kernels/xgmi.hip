@@ -156,19 +156,25 @@ __device__ __forceinline__ void unpack8_bf16(uint4 u, float4& a, float4& b) {
 struct XRange {
   int64_t va, vb;  // vector body in units
 };
+// Body units [ceil(a/U), floor(b/U)), empty when [a, b) holds no whole unit (then vb = va).  The
+// edges are [a, min(b, va*U)) and [max(vb*U, min(b, va*U)), b): disjoint, inside [a, b), and
+// together with the body exactly [a, b) -- also when the range sits inside one unit at an
+// unaligned offset (a = 5, b = 7 with U = 4: left edge 5, 6; no body; no right edge).
 template <int U>
 __device__ __forceinline__ XRange xrange(int64_t a, int64_t b) {
-  const int64_t va = (a + U - 1) / U * U < b ? (a + U - 1) / U * U : b;
-  const int64_t vb = b / U * U > va ? b / U * U : va;
-  return {va / U, vb / U};
+  const int64_t va = (a + U - 1) / U;
+  const int64_t vb = b / U > va ? b / U : va;
+  return {va, vb};
 }
 template <int U, class F>
 __device__ __forceinline__ void xedges(int64_t a, int64_t b, F&& f) {
   const XRange r = xrange<U>(a, b);
   const int t = threadIdx.x;
   if (blockIdx.x == 0 && t < U) {
-    if (a + t < r.va * U) f(a + t);
-    if (r.vb * U + t < b) f(r.vb * U + t);
+    const int64_t lend = b < r.va * U ? b : r.va * U;
+    const int64_t rbeg = r.vb * U > lend ? r.vb * U : lend;
+    if (a + t < lend) f(a + t);
+    if (rbeg + t < b) f(rbeg + t);
   }
 }
 

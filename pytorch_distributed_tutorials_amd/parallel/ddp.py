@@ -142,7 +142,7 @@ class DistributedDataParallel(nn.Module):
                  find_unused_parameters: bool = False, gradient_as_bucket_view: bool = True,
                  comm: str = "auto", wire_dtype: str = "fp32", average: bool = True,
                  last_bucket_mb="auto", force_reducer: bool = False,
-                 comm_options: Optional["pcomm.CommOptions"] = None):
+                 comm_options: Optional["pcomm.CommOptions"] = None, plan_world: Optional[int] = None):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -182,9 +182,14 @@ class DistributedDataParallel(nn.Module):
             if self.last_bucket_mb != "auto":
                 raise ValueError(f"last_bucket_mb must be a number, None or 'auto', got {self.last_bucket_mb!r}")
             # the last bucket's all-reduce is the one nothing hides: cap it where the tail model
-            # says the step is shortest (None at world 1: no all-reduce to hide)
-            self.last_bucket_mb = auto_last_bucket_mb(sizes, self.world_size, self.bucket_cap_mb,
+            # says the step is shortest (None at world 1: no all-reduce to hide).  plan_world: the
+            # world size the layout is planned for -- a world-1 force_reducer run passes the node's
+            # rank count so one GPU executes the multi-GPU bucket layout (tail bucket included)
+            self.plan_world = int(plan_world) if plan_world else self.world_size
+            self.last_bucket_mb = auto_last_bucket_mb(sizes, self.plan_world, self.bucket_cap_mb,
                                                       self.first_bucket_mb)
+        else:
+            self.plan_world = int(plan_world) if plan_world else self.world_size
         plan = ddp_bucket_plan(sizes, self.bucket_cap_mb, self.first_bucket_mb, self.last_bucket_mb)
         layout = [i for b in plan for i in b]
         self.comm_options = comm_options or pcomm.CommOptions.from_env()

@@ -1,0 +1,188 @@
+"""Worker for tests/test_multigpu_gpu.py: one process per GPU on SEPARATE devices (cuda:local_rank).
+
+The one-GPU boxes run every multi-rank test with the ranks sharing cuda:0 (gloo, same-device IPC,
+world-1 RCCL communicators).  These modes are what only a node with >= 2 GPUs can execute --
+RCCL between devices, xGMI peer mappings between devices, and data-parallel training whose
+ranks live on different GPUs -- so the first multi-GPU box a run lands on verifies them:
+
+* ``rccl``: our RCCL communicator (``parallel.comm.native_comm``, unique id over the store)
+  across the devices: all_reduce sum / avg and broadcast against gloo on the same data (exact on
+  integer-valued data, within fp32 reassociation on random data);
+* ``xgmi``: ``XgmiComm`` with peer buffers on other GPUs: buckets (aligned, odd offsets, tiny
+  unaligned) against the rank-order fp32 sum bitwise, then the POISON protocol (rank 0 times out
+  waiting for late peers; every late peer fails with "peer rank 0 failed first"; NaN buckets);
+* ``ddp``: native ResNet-18 under ``DistributedDataParallel`` over RCCL (and, with ``--comm
+  xgmi``, the direct backend), a few SGD steps; parameter checksums all-gathered: every rank
+  bit-identical.
+
+Prints one RESULT json line per rank.
+"""
+import argparse
+import json
+import os
+import sys
+import traceback
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from pytorch_distributed_tutorials_amd.parallel import init_distributed  # noqa: E402
+
+
+def _gather_cpu(t):
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return out
+
+
+def run_rccl(rank, world, dev):
+    from pytorch_distributed_tutorials_amd.parallel.comm import native_comm
+    comm = native_comm(dev)
+    res = {"comm_count": comm.comm_count()}
+    n = 1 << 20
+    g = torch.Generator().manual_seed(10 + rank)
+    ints = torch.randint(-1000, 1000, (n,), generator=g).float()
+    rnd = torch.randn(n, generator=g)
+    # integer-valued fp32: every summation order is exact -> bitwise against gloo
+    t = ints.to(dev)
+    comm.all_reduce(t, "sum")
+    comm.synchronize()
+    ref = ints.clone()
+    dist.all_reduce(ref)
+    res["sum_exact"] = bool(torch.equal(t.cpu(), ref))
+    t = rnd.to(dev)
+    comm.all_reduce(t, "avg")
+    comm.synchronize()
+    ref = rnd.clone()
+    dist.all_reduce(ref)
+    ref /= world
+    res["avg_max_abs"] = float((t.cpu() - ref).abs().max())
+    src = 1 % world
+    b = (rnd * (rank + 1)).to(dev)
+    comm.broadcast(b, src)
+    comm.synchronize()
+    want = _gather_cpu(rnd * (rank + 1))[src]
+    res["broadcast_exact"] = bool(torch.equal(b.cpu(), want))
+    return res
+
+
+def run_xgmi(rank, world, dev):
+    from pytorch_distributed_tutorials_amd.parallel.xgmi import xgmi_comm
+    n = (1 << 20) + 77
+    buckets = [(0, 400000), (400000, 300001), (700001, 5), (700006, 2), (700013, 348000)]
+    comm = xgmi_comm(dev, n, len(buckets), timeout=60.0, exit_on_error=False)
+    buf = comm.grad_buffer()
+    res = {"bitwise_vs_rank_order": True, "untouched_kept": True}
+    for epoch in range(2):
+        gen = torch.Generator().manual_seed(1000 * epoch + rank)
+        mine = torch.randn(n, generator=gen)
+        buf.copy_(mine.to(dev))
+        torch.cuda.synchronize()
+        for bi, (off, cnt) in enumerate(buckets):
+            comm.reduce_bucket(bi, off, cnt, True)
+        comm.synchronize()
+        got = buf.cpu()
+        alls = _gather_cpu(mine)
+        ordered = alls[0].clone()
+        for q in range(1, world):
+            ordered += alls[q]
+        ordered /= world
+        covered = torch.zeros(n, dtype=torch.bool)
+        for off, cnt in buckets:
+            covered[off:off + cnt] = True
+        res["bitwise_vs_rank_order"] &= bool(torch.equal(got[covered], ordered[covered]))
+        res["untouched_kept"] &= bool(torch.equal(got[~covered], mine[~covered]))
+    res["error_code"] = comm.error_code
+    res["flags_uncached"] = bool(comm.flags_uncached)
+    del comm
+    torch.cuda.synchronize()
+    # POISON: rank 0 arrives first and times out on its late peers; each late peer then fails
+    # with rank 0's POISON instead of gathering a shard that was never reduced
+    m = 8192
+    pc = xgmi_comm(dev, m, 1, timeout=0.5, exit_on_error=False)
+    pc.grad_buffer().fill_(float(rank + 1))
+    torch.cuda.synchronize()
+    msg = ""
+    if rank == 0:
+        pc.reduce_bucket(0, 0, m, True)
+        try:
+            pc.synchronize()
+        except RuntimeError as e:
+            msg = str(e)
+        dist.barrier()
+    else:
+        dist.barrier()
+        pc.reduce_bucket(0, 0, m, True)
+        try:
+            pc.synchronize()
+        except RuntimeError as e:
+            msg = str(e)
+    res["poison_msg"] = msg[:300]
+    res["poison_nan"] = bool(torch.isnan(pc.grad_buffer()).all())
+    res["poison_code"] = int(pc.error_code)
+    dist.barrier()
+    return res
+
+
+def run_ddp(rank, world, dev, comm_kind, steps=3):
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    from pytorch_distributed_tutorials_amd.optim import SGD
+    from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    m = build_model("resnet18", num_classes=10).to(dev).set_impl("native")
+    ddp = DistributedDataParallel(m, device_ids=[dev.index], comm=comm_kind)
+    opt = SGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-5)
+    gen = torch.Generator().manual_seed(77 + rank)
+    losses = []
+    for _ in range(steps):
+        x = torch.randn(16, 3, 32, 32, generator=gen).to(dev)
+        y = torch.randint(0, 10, (16,), generator=gen).to(dev)
+        opt.zero_grad()
+        loss = ops.cross_entropy(ddp(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.item()))
+    torch.cuda.synchronize()
+    flat = ddp.space.param_flat.detach()
+    bits = flat.view(torch.int32).to(torch.int64)
+    idx = torch.arange(bits.numel(), device=dev, dtype=torch.int64)
+    cs = int((bits * (idx % 8191 + 1)).sum().item())
+    info = ddp.bucket_info()
+    return {"checksum": cs, "losses": losses, "finite": all(l == l for l in losses),
+            "native_comm": info["native_comm"], "xgmi": info["xgmi"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", required=True, choices=["rccl", "xgmi", "ddp"])
+    ap.add_argument("--comm", default="auto", choices=["auto", "xgmi"])
+    a = ap.parse_args()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)  # before any process group (reference defect D9)
+    dev = torch.device("cuda", local)
+    env = init_distributed("nccl" if a.mode == "ddp" else "gloo", local_rank=local)
+    out = {"rank": env.rank, "world": env.world_size, "device": local}
+    try:
+        if a.mode == "rccl":
+            out.update(run_rccl(env.rank, env.world_size, dev))
+        elif a.mode == "xgmi":
+            out.update(run_xgmi(env.rank, env.world_size, dev))
+        else:
+            out.update(run_ddp(env.rank, env.world_size, dev, a.comm))
+        out["status"] = "ok"
+    except Exception as e:  # noqa: BLE001 -- reported in the RESULT line
+        out["status"] = "error"
+        out["error"] = f"{type(e).__name__}: {e}"
+        out["trace"] = traceback.format_exc()[-2000:]
+    print("RESULT " + json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.stdout.flush()
+    os._exit(0 if out["status"] == "ok" else 1)
+
+
+if __name__ == "__main__":
+    main()

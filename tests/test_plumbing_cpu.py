@@ -245,6 +245,8 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
     assert d["config"]["global_batch"] == 8 and d["config"]["parallelism"] == "dp2"
     assert abs(d["value"] - 8 * 2 / (d["ms_per_step"] * 2 / 1000.0)) / d["value"] < 1e-2
+    # every rank ends with bit-identical parameters (all-gathered checksum)
+    assert d["config"]["ranks_identical"] is True and isinstance(d["config"]["param_checksum"], int)
 
 
 def test_bench_two_ranks_native_reports_comm_diagnostics(tmp_path):
@@ -266,7 +268,9 @@ def test_bench_two_ranks_native_reports_comm_diagnostics(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
-    c = json.loads(lines[0])["config"]["comm"]
+    cfg = json.loads(lines[0])["config"]
+    assert cfg["ranks_identical"] is True and cfg["plan_world"] == 2
+    c = cfg["comm"]
     assert c["world_size"] == 2 and c["comm_count"] == 2 and c["count_matches_world"]
     assert c["backend"] == "python-gloo" and c["wire_dtype"] == "fp32"
     assert len(c["buckets_mb"]) >= 2 and all(b > 0 for b in c["buckets_mb"])

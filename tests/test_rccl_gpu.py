@@ -334,7 +334,13 @@ def test_bench_force_comm_reports_diagnostics(gpu, tmp_path):
                         "--batch", "32", "--steps", "2", "--warmup", "1", "--force-comm", "--json-out", str(out)],
                        cwd=ROOT, timeout=300, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    c = json.loads(out.read_text())["config"]["comm"]
+    cfg = json.loads(out.read_text())["config"]
+    # a world-1 --force-comm run executes the 8-rank bucket layout, tail bucket
+    # included (auto_last_bucket_mb planned for 8 ranks), and reports the parameter checksum
+    assert cfg["plan_world"] == 8 and cfg["last_bucket_mb"] is not None
+    assert cfg["comm"]["buckets_mb"][-1] <= cfg["last_bucket_mb"] + 1e-6
+    assert cfg["ranks_identical"] is True
+    c = cfg["comm"]
     assert c["backend"] == "rccl" and c["native_comm"] and c["comm_count"] == 1 and c["count_matches_world"]
     assert c["rccl_version"] >= 20000 and c["healthy"]
     assert c["comm_ms"] >= 0 and 0 <= c["exposed_ms"] <= c["comm_ms"] + 1e-3

@@ -135,9 +135,15 @@ def test_dgrad_and_bn_dgrad_per_tile(gpu, native_ext, shape, tile):
 
 
 WGRAD_PLANS = [
-    ((16, 56, 56, 64, 256, 1, 1, 1, 0), 128),    # pointwise wgrad, 128-row tile
-    ((16, 56, 56, 64, 64, 3, 3, 1, 1), 64),      # Kout = 64: 64-row tile
+    ((16, 56, 56, 64, 256, 1, 1, 1, 0), 256),    # pointwise wgrad, 64 input channels: 256x64 tile
+    ((16, 56, 56, 256, 128, 1, 1, 1, 0), 128),   # pointwise wgrad, 128x128 tile
+    ((16, 56, 56, 64, 64, 3, 3, 1, 1), 64),      # Kout = 64: 64x256 tile, general loader
     ((16, 28, 28, 256, 512, 1, 1, 2, 0), 128),   # strided 1x1 (general loader)
+    ((8, 7, 7, 512, 512, 3, 3, 1, 1), 128),      # 3x3 halo kernel, 7x7: 47 % padded q-rows
+    ((16, 28, 28, 128, 128, 3, 3, 1, 1), 128),   # 3x3 halo kernel, 128x(3x64) tile
+    ((2, 14, 14, 192, 256, 3, 3, 1, 1), 128),    # 3x3 halo kernel, 3 channel blocks, 2 images
+    ((3, 9, 5, 64, 64, 3, 3, 1, 1), 64),         # 3x3 halo kernel, tiny odd image (steps span images)
+    ((4, 14, 14, 72, 40, 3, 3, 2, 1), 64),       # ragged: Kout / columns not tile multiples
 ]
 
 
@@ -148,9 +154,18 @@ def test_wgrad_per_plan(gpu, native_ext, shape, bm, det):
     n, h, w, c, k, r, s, st, pd = shape
     x, wt, dy = _operands(shape, gpu, 4)
     plan = C.conv_wgrad_plan(list(x.shape), list(wt.shape), st, pd, det)
-    assert plan["bm"] == bm and plan["splits"] > 1
+    assert plan["bm"] == bm
+    assert plan["splits"] > 1 or n * h * w // (st * st) < 64 * 4 * 8  # only tiny reductions stay unsplit
     dw = C.conv_wgrad(dy, x, list(wt.shape), st, pd, det)
-    assert _rel(dw, ref.conv2d_nhwc_wgrad(dy, x, wt.shape, st, pd)) < 1e-2
+    dw_ref = ref.conv2d_nhwc_wgrad(dy, x, wt.shape, st, pd)
+    assert _rel(dw, dw_ref) < 1e-2
+    # accumulated into a KRSC sink (the flat-gradient path: atomics, slabs + reduce, or += store)
+    sink = torch.randn(k, r, s, c, device=gpu).permute(0, 3, 1, 2)
+    base = sink.clone()
+    C.conv_wgrad(dy, x, list(wt.shape), st, pd, det, sink)
+    assert _rel(sink - base, dw_ref) < 1e-2
+    if det:  # slab split-K + fixed-order reduce: bitwise run to run
+        assert torch.equal(C.conv_wgrad(dy, x, list(wt.shape), st, pd, det), dw)
 
 
 def _deq(q, fmt):

@@ -54,6 +54,8 @@ def test_xgmi_in_process_ranks_bitwise(gpu, world):
             assert torch.equal(got[:end], ref[:end]), (world, epoch, q, float((got[:end] - ref[:end]).abs().max()))
             assert torch.equal(got[end:], data[q][end:])   # outside every bucket: untouched
     assert all(c.error_code == 0 for c in comms)
+    # the cross-GPU epoch flags live in uncached (fine-grained) memory
+    assert all(c.flags_uncached for c in comms)
 
 
 def test_xgmi_sum_without_average(gpu):
@@ -112,6 +114,37 @@ def test_xgmi_unaligned_buckets_and_cu_budget(gpu, wire):
                 assert float(err.max()) < 3 * 2 ** -8 * float(ref[:end].abs().max() + 1), (blocks, q)
             assert torch.equal(got[end:], data[q][end:])
         del comms
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_xgmi_tiny_unaligned_buckets_leave_neighbours_alone(gpu, wire):
+    # buckets shorter than one vector unit at unaligned offsets (4 elements fp32 wire, 8 bf16): the
+    # edge split must stay inside [a, b) -- round 4's xrange let (5, 2) touch element 4
+    from pytorch_distributed_tutorials_amd.parallel.xgmi import local_group, reduce_local_group
+    n = 64
+    buckets = [(5, 2), (9, 5), (17, 3), (21, 1), (30, 11)]
+    comms = local_group(gpu, n, len(buckets), 2, timeout=20.0, wire=wire)
+    g = torch.Generator().manual_seed(7)
+    data = [torch.randn(n, generator=g) for _ in range(2)]
+    for c, d in zip(comms, data):
+        c.grad_buffer().copy_(d.to(gpu))
+    torch.cuda.synchronize()
+    for bi, (off, cnt) in enumerate(buckets):
+        reduce_local_group(comms, bi, off, cnt, True)
+    for c in comms:
+        c.synchronize()
+    inside = torch.zeros(n, dtype=torch.bool)
+    for off, cnt in buckets:
+        inside[off:off + cnt] = True
+    ref = (data[0] + data[1]) / 2
+    for q, c in enumerate(comms):
+        got = c.grad_buffer().cpu()
+        assert torch.equal(got[~inside], data[q][~inside]), (wire, q)
+        if wire == "fp32":
+            assert torch.equal(got[inside], ref[inside]), q
+        else:
+            assert float((got[inside] - ref[inside]).abs().max()) < 3 * 2 ** -8 * float(ref.abs().max() + 1), q
+    del comms
 
 
 def test_xgmi_bf16_wire_error_at_8_ranks(gpu):
