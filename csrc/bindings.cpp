@@ -507,15 +507,6 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
 // -------------------------------------------------------------------- stem
 // 7x7/s2 stem with C <= 4 input channels as a super-pixel conv (kernels.h): returns
 // (xsp, y, part) -- xsp is the bf16 super-pixel image (kept for the weight gradient)
-static bool stem_halo_mode() {  // PDT_STEM_HALO=0: the generic super-pixel implicit GEMM (A/B knob)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_STEM_HALO");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
 std::tuple<Tensor, Tensor, Tensor, int64_t> stem_conv_fwd(const Tensor& x, const Tensor& w, int64_t stride,
                                                           int64_t pad, bool stats) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "stem: image must be fp32 NCHW");
@@ -542,7 +533,7 @@ std::tuple<Tensor, Tensor, Tensor, int64_t> stem_conv_fwd(const Tensor& x, const
   Tensor part;
   float* pp = nullptr;
   const int M = N * Ho * Wo;
-  const bool halo = stem_halo_mode() && pdt::stem_halo_supported(K, R, Sp, Wo);
+  const bool halo = pdt::stem_halo_supported(K, R, Sp, Wo);
   // BN partial groups: one per output row on the halo kernel, one per NT row tile otherwise
   const int grows = halo ? Wo : pdt::conv_nt_group_rows(M, K, R * Sp * 8 * 2);
   if (stats) {
@@ -1412,7 +1403,6 @@ PYBIND11_MODULE(_C, m) {
     const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
     return out.narrow(0, 0, got);
   }, py::arg("n"));
-  m.def("conv_stream_k_launches", []() { return pdt::conv_stream_k_launches(); });
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);

@@ -40,12 +40,8 @@ std::string RcclComm::unique_id() {
 // The comm stream is an ordinary-priority stream.  A high-priority stream was measured to cost
 // +16.5 ms per ResNet-50 step on MI355X (21.6 -> 38.1 ms, world-1 forced reducer) even with the
 // collectives skipped (PDT_REDUCER_SKIP_COLL=1: 38.0 ms): its event waits, not RCCL, stall the
-// compute queues.  PDT_COMM_HIGH_PRIORITY=1 restores it for A/B runs
-// (profiles/r2_comm_stream_priority_ab.md).
-static bool comm_high_priority() {
-  const char* e = std::getenv("PDT_COMM_HIGH_PRIORITY");
-  return e && e[0] == '1';
-}
+// compute queues.  Measured: profiles/r2_comm_stream_priority_ab.md.
+static bool comm_high_priority() { return false; }
 
 // Communicator mode.  Default: a BLOCKING communicator whose init runs on a helper thread that
 // the constructor waits for with a deadline.  A non-blocking communicator (PDT_RCCL_NONBLOCKING=1)

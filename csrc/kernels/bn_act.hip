@@ -334,21 +334,7 @@ static int ew_block_cap_env() {
 constexpr int kEwCap = 8192;
 constexpr int kEwCapResidual = 32768;
 
-// PDT_EW_UNROLL = U (1, 2 or 4): the bn_act_fwd / bn_bwd_apply passes keep U 16-byte vectors of
-// every operand in flight per thread (loads batched ahead of the math and the stores), on a grid
-// of at most one resident wave per slot (2048 blocks).  Default 1: the round-3 grid-stride form.
-static int ew_unroll() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_EW_UNROLL");
-    v = e ? atoi(e) : 1;
-    v = (v == 2 || v == 4) ? v : 1;
-  }
-  return v;
-}
-
 static int ew_blocks(int64_t nvec, int K8, int cap_default = kEwCap) {
-  if (ew_unroll() > 1) cap_default = 2048;  // resident blocks of 256 threads (8 per CU)
   int64_t b = (nvec + 255) / 256;
   const int64_t cap = ew_block_cap_env() > 0 ? ew_block_cap_env() : cap_default;
   b = b < cap ? b : cap;
@@ -360,19 +346,8 @@ template <bool RES, bool RELU, bool MASK, bool RESBN>
 static void fwd_launch(dim3 g, dim3 b, hipStream_t st, const uint4* Y, const float* scale, const float* shift,
                        const uint4* R, uint4* Z, int64_t nvec, int K8, uint8_t* zmask = nullptr,
                        const float* rscale = nullptr, const float* rshift = nullptr) {
-  switch (ew_unroll()) {
-    case 4:
-      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 4>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
-                         zmask, rscale, rshift);
-      break;
-    case 2:
-      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 2>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
-                         zmask, rscale, rshift);
-      break;
-    default:
-      hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 1>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
-                         zmask, rscale, rshift);
-  }
+  hipLaunchKernelGGL((bn_act_fwd_kernel<RES, RELU, MASK, RESBN, 1>), g, b, 0, st, Y, scale, shift, R, Z, nvec, K8,
+                     zmask, rscale, rshift);
 }
 
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
@@ -750,16 +725,10 @@ void launch_bn_act_bwd_apply(const uint16_t* dz, const uint16_t* z, const uint16
   auto DY = reinterpret_cast<uint4*>(dy);
   auto DR = reinterpret_cast<uint4*>(dres);
   float invM = 1.f / (float)M;
-  const int unr = ew_unroll();
 #define PDT_BWD_U(MK, TR, DRS, UU)                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<MK, TR, DRS, false, UU>), g, b, 0, st, DZ, Z, Y, stats, gamma, \
                      sums, nvec, K8, invM, DY, DR, nullptr, nullptr, 0, dgamma, dbeta)
-#define PDT_BWD(MK, TR, DRS)                                            \
-  do {                                                                  \
-    if (unr == 4) PDT_BWD_U(MK, TR, DRS, 4);                            \
-    else if (unr == 2) PDT_BWD_U(MK, TR, DRS, 2);                       \
-    else PDT_BWD_U(MK, TR, DRS, 1);                                     \
-  } while (0)
+#define PDT_BWD(MK, TR, DRS) PDT_BWD_U(MK, TR, DRS, 1)
 #define PDT_BWD_T(MK)                                                             \
   if (training) { if (dres) PDT_BWD(MK, true, true); else PDT_BWD(MK, true, false); } \
   else { if (dres) PDT_BWD(MK, false, true); else PDT_BWD(MK, false, false); }

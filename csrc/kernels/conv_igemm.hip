@@ -1087,7 +1087,7 @@ struct NtqCfg {
 
 // OP: bf16 (a 128-B K-step = 64 elements = two 16x16x32 MFMAs per tile pair) or fp8 (128
 // elements = one MX-rate 16x16x128 MFMA, operand = 32 B per lane: chunks 2fq, 2fq+1)
-template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16, bool PIPE = false>
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
 __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_WAVES))
     igemm_ntq_kernel(const NtArgs P) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
@@ -1242,7 +1242,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   };
 
   v4i x0[TMQ][2], x1[TMQ][2], w0f[TNQ][2], w1f[TNQ][2];
-  if constexpr (!PIPE) {
   for (int s = 0; s < nk; ++s) {
     const int st = s & 1;
     const char* base = smem + st * STAGE;
@@ -1271,695 +1270,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
     advance();
     mma(TMQ, TNQ, x1, w1f);
   }
-  } else {
-  // PIPE: every phase's fragment reads are issued one phase EARLY, right after that phase's
-  // barrier, and land while this phase's MFMAs run (the reads of a phase no longer wait behind
-  // its own barrier):  P0 reads W1(s) | P1 reads X1(s) | P2 none | P3 reads X0, W0 of step s+1
-  // (x0 / w0f are dead after P1 / P2).  Waits per phase (glds younger than the quarters read):
-  // P0 W1(s): 10, P1 X1(s): 8, P3 X0, W0(s+1): 10.  Refills as above (X0, W0 at P1, W1 at P2, X1
-  // at P3); each refill's slot was last read one phase earlier, retired by that phase's barrier.
-  wait_vm<12>();
-  lds_barrier_rd();
-  read_x(smem, x0);
-  read_w(smem + 2 * QX, w0f);
-  for (int s = 0; s < nk; ++s) {
-    const int st = s & 1;
-    const char* base = smem + st * STAGE;
-    const char* nbase = smem + (st ^ 1) * STAGE;
-    // P0: Q(0,0) from x0 / w0f; read W1(s)
-    wait_vm<10>();
-    lds_barrier_rd();
-    read_w(base + 2 * QX + QW, w1f);
-    mma(0, 0, x0, w0f);
-    // P1: Q(0,1); X0, W0 slots (read at P3 of step s-1) -> step s+2; read X1(s)
-    wait_vm<8>();
-    lds_barrier_rd();
-    issue(0, 0, st);
-    issue(1, 0, st);
-    read_x(base + QX, x1);
-    mma(0, TNQ, x0, w1f);
-    // P2: Q(1,0); W1 slot (read at P0) -> step s+2
-    lds_barrier_rd();
-    issue(1, 1, st);
-    mma(TMQ, 0, x1, w0f);
-    // P3: Q(1,1); X1 slot (read at P1) -> step s+2; read X0, W0 of step s+1
-    wait_vm<10>();
-    lds_barrier_rd();
-    issue(0, 1, st);
-    advance();
-    read_x(nbase, x0);
-    read_w(nbase + 2 * QX, w0f);
-    mma(TMQ, TNQ, x1, w1f);
-  }
-  }
   wait_vm<0>();
   lds_barrier_rd();  // every DMA landed and every fragment read done before the epilogue reuses LDS
   nt_epilogue<CFG, WM, WN, 2 * TMQ, 2 * TNQ, EPI, OP>(P, acc, smem, m0, n0, tmi);
-}
-
-// ============================================================================
-//        NT 256x256, ping-pong wave groups (long-K fwd / dgrad, bf16)
-// ============================================================================
-// Two wave groups share every SIMD (waves w and w+4; G0 = waves 0-3, G1 = waves 4-7) and run the
-// same program one segment apart, so while one wave of a SIMD issues its MFMAs the other issues
-// its LDS-DMA pieces and fragment reads (MI355X_MICROARCH "Two waves per SIMD"; the structure of
-// the 256x256 8-phase template in cdna_hip_programming.md 5):
-//     wave:  L_0 | C_0 | L_1 | C_1 | ...        (| = workgroup barrier)
-//     G0     L   | C   | L   | C   | ...
-//     G1     -   | L   | C   | L   | C ...      (one extra barrier before its first segment)
-// A segment works on one K32 half-step m (32 channels of one tap): L_m issues this wave's 4 DMA
-// pieces of half m+3 into ring slot (m+3) % 4 (= slot m-1, read by both groups' L_{m-1}, which
-// are both behind this L in barrier order), reads the wave's 12 fragments of half m, and waits
-// (vmcnt 8: halves m+2, m+3 may stay in flight) for its own pieces of half m+1 before the
-// barrier; C_m runs the wave's 32 MFMAs.  RAW: half m+1 is read first by G0's L_{m+1}, one
-// barrier after BOTH groups' L_m waits.  Every half is issued 3 L-segments (~4 MFMA segments of
-// the SIMD) before its first read.  Slots: [X 256 rows x 64 B][W 256 rows x 64 B] = 32 KB, 4 slots.
-// Wave tiles as igemm_ntq's epilogue wants them: (wm = wid % 2) 128 rows x (wn = wid / 2) 64 cols.
-// K64 = true: K64 steps in 2 stages of [X 256 x 128 B][W 256 x 128 B] (full 128-B rows: one global
-// line per row), segments = the two k-sub-steps of a step.  L(k, 0) (k >= 1) issues step k+1 into
-// stage (k+1) & 1 = (k-1) & 1 (last read by G1's L(k-1, 1), one barrier earlier); L(k, 1) ends
-// with vmcnt(0) for it, so a piece has ~3 segments to land instead of ~5 (K32 ring).
-// Stream-K (SK = true), for grids of fewer 256x256 tiles than CUs (the long-K 3x3 / 1x1 shapes of
-// the 14x14 and 7x7 stages: 196 and 98 tiles on 256 CUs).  The (tile, K-unit) iteration space,
-// tile-major, is cut into gridDim.x equal contiguous ranges, one per workgroup.  A range starts
-// with the tail of one tile (unless it starts on a tile boundary), continues over whole tiles and
-// ends with the head of another.  The workgroup that runs a tile's first unit owns the tile: it
-// adds the fp32 partial sums of the workgroups whose ranges start inside the tile (in workgroup
-// order: deterministic) and runs the normal epilogue.  A contributor stores its partial once, in
-// its own 256 KB workspace slot (lane-native order: one float4 per lane and accumulator tile),
-// publishes it (device-scope stores, vmcnt(0), barrier, flag = 1); the owner polls each flag,
-// resets it to 0 (the next launch starts from zeros, also under graph replay) and reads the slot
-// with device-scope loads.  Owners wait
-// only on HIGHER workgroup ids, whose partial is the FIRST thing they compute; every workgroup is
-// resident at once (grid <= CUs, one workgroup per CU), so the waits end.
-// Partials cross XCDs (each XCD has its own L2): contributors store and owners load them with the
-// device-scope cache policy (SC1), so no L2-wide writeback / invalidate is needed around the flags.
-constexpr int kCpolSc1 = 16;
-constexpr int kSkMaxParts = 2;  // partials one owner adds (the launcher keeps per_wg >= nu / 2)
-
-struct NtpSk {
-  float* ws;          // [gridDim.x][8 waves][32 tiles][64 lanes][4]
-  uint32_t* flags;    // [gridDim.x]
-  int per_wg;         // K-units per workgroup range
-  uint32_t ws_bytes;
-};
-
-template <int EPI, bool K64, bool SK>
-__global__ void __launch_bounds__(512, 1) igemm_ntp_kernel(const NtArgs P, const NtpSk S) {
-  using CFG = NtCfg<2, 4, 8, 4, 2, false>;
-  static_assert(CFG::BM == 256 && CFG::BN == 256, "ntp geometry");
-  constexpr int EB = 2;
-  constexpr int ROWB = K64 ? 128 : 64;     // bytes per tile row in LDS
-  constexpr int KH = ROWB / EB;            // channels per DMA unit (step or half)
-  constexpr int SLOT = 2 * 256 * ROWB;     // 64 KB stage / 32 KB half slot
-  constexpr int NSLOT = K64 ? 2 : 4;
-  constexpr int LPR = ROWB / 16, RPP = 64 / LPR;  // lanes per row, rows per 1-KiB piece
-  constexpr int PP = 256 / RPP / 8;               // pieces per operand per wave: 4 (K64) / 2 (K32)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int ntn = (P.Nout + 255) / 256;
-  const int ntm = (P.M + 255) / 256;
-  const int t = threadIdx.x;
-  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const bool g1 = wid >= 4;
-  const int lr = lane / LPR, lj = lane % LPR;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
-  auto rd_off = [](int row, int chunk) {
-    if constexpr (K64) return swz128(row, chunk);
-    else return swz64(row, chunk);
-  };
-  const int upc = P.CA / KH;               // units per tap
-  const int nu = P.ntaps * upc;            // units per tile
-  const int wm = wid % 2, wn = wid / 2;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  // units [ub, ue) of tile (tmi, tni) into acc (which the caller zeroed)
-  auto tile_loop = [&](int m0, int n0, int ub, int ue, v4f (&acc)[8][4]) {
-    // this lane's DMA rows: piece p covers tile rows r = (wid*PP + p)*RPP + lr of X and of W
-    int a_base[PP], b_row[PP], b_c[PP];
-    uint32_t a_inv[PP];
-#pragma unroll
-    for (int p = 0; p < PP; ++p) {
-      const int r = (wid * PP + p) * RPP + lr;
-      const int sc = K64 ? (lj ^ ((r >> 1) & 7)) : (lj ^ swz64_g(r));  // source chunk landing in slot lj
-      b_c[p] = sc;
-      const int m = m0 + r;
-      int pix = 0, h0 = -(1 << 20), w0 = 0;
-      if (m < P.M) {
-        const uint32_t n = fdiv((uint32_t)m, P.div_ij);
-        const uint32_t rem = (uint32_t)m - n * (uint32_t)P.Mij;
-        const uint32_t ii = fdiv(rem, P.div_j);
-        const uint32_t jj = rem - ii * (uint32_t)P.Mj;
-        pix = (int)n * P.HA * P.WA;
-        h0 = (int)ii * P.ash + P.aoff_h;
-        w0 = (int)jj * P.asw + P.aoff_w;
-      }
-      a_base[p] = (pix + h0 * P.WA + w0) * P.CA * EB + sc * 16;
-      const int nr = P.tnr, ns = P.tns;
-      const int hb = h0 + P.dr0, wb = w0 + P.ds0;
-      const int hlo = P.dstep > 0 ? max(0, -hb) : max(0, hb - P.HA + 1);
-      const int hhi = P.dstep > 0 ? min(nr, P.HA - hb) : min(nr, hb + 1);
-      const int wlo = P.dstep > 0 ? max(0, -wb) : max(0, wb - P.WA + 1);
-      const int whi = P.dstep > 0 ? min(ns, P.WA - wb) : min(ns, wb + 1);
-      const uint32_t hm = hhi > hlo ? (1u << (hhi & 31)) - (1u << (hlo & 31)) : 0u;
-      const uint32_t wmk = whi > wlo ? (1u << (whi & 31)) - (1u << (wlo & 31)) : 0u;
-      uint32_t spread = 0u;
-      for (int ti = 0; ti < nr; ++ti) spread |= ((hm >> ti) & 1u) << (ti * ns);
-      a_inv[p] = ~(wmk * spread);
-      const int ch = n0 + r;
-      b_row[p] = ch < P.Nout ? ch * P.Kg : -1;
-    }
-
-    // state of the NEXT unit to issue: tap row, tap column, channel offset, unit index
-    const int tap0 = ub / upc;
-    int q_ti = tap0 / P.tns, q_tj = tap0 - (tap0 / P.tns) * P.tns, q_chb = (ub - tap0 * upc) * KH;
-    int q_u = 0;  // relative to ub
-    const int n_u = ue - ub;
-    auto issue_next = [&]() {
-      const bool valid = q_u < n_u;
-      char* slot = smem + (q_u % NSLOT) * SLOT;
-      const int tap = q_ti * P.tns + q_tj;
-      const int dr = P.dr0 + q_ti * P.dstep, ds = P.ds0 + q_tj * P.dstep;
-      const int tdelta = ((dr * P.WA + ds) * P.CA + q_chb) * EB;
-      const int tbo = ((P.tr0 + q_ti * P.tstep) * P.S + (P.ts0 + q_tj * P.tstep)) * P.CA + q_chb;
-#pragma unroll
-      for (int p = 0; p < PP; ++p) {
-        const uint32_t poison = (uint32_t)__builtin_amdgcn_sbfe((int)a_inv[p], (unsigned)tap, 1u) |
-                                (valid ? 0u : 0xffffffffu);
-        glds16(ra, slot + (wid * PP + p) * 1024, (uint32_t)(a_base[p] + tdelta) | poison);
-      }
-#pragma unroll
-      for (int p = 0; p < PP; ++p) {
-        const uint32_t off = (valid && b_row[p] >= 0) ? (uint32_t)((b_row[p] + tbo) * EB + b_c[p] * 16) : OOB;
-        glds16(rb, slot + SLOT / 2 + (wid * PP + p) * 1024, off);
-      }
-      ++q_u;
-      q_chb += KH;
-      if (q_chb == P.CA) {
-        q_chb = 0;
-        if (++q_tj == P.tns) { q_tj = 0; ++q_ti; }
-      }
-    };
-
-    // prologue: K64 -- units 0, 1; K32 -- halves 0, 1, 2.  Unit 0 landed everywhere before the reads.
-    issue_next();
-    issue_next();
-    if constexpr (!K64) issue_next();
-    wait_vm<K64 ? 2 * PP : 4 * PP>();
-    lds_barrier_rd();
-    if (g1) {
-      __builtin_amdgcn_s_setprio(1);  // the younger group: static priority (MI355X_MICROARCH item 4)
-      lds_barrier();                  // one segment behind G0
-    }
-    const int nh = K64 ? 2 * n_u : n_u;  // segments
-    v4i xf[8], wf[4];
-    for (int m = 0; m < nh; ++m) {
-      // L_m
-      const char* xs;
-      int ck;
-      if constexpr (K64) {
-        const int k = m >> 1, ks = m & 1;
-        if (ks == 0 && k >= 1) issue_next();  // unit k + 1
-        xs = smem + (k & 1) * SLOT;
-        ck = ks * 4 + fq;
-      } else {
-        issue_next();  // half m + 3 into slot (m + 3) % 4
-        xs = smem + (m & 3) * SLOT;
-        ck = fq;
-      }
-      const char* ws = xs + SLOT / 2;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) xf[i] = *reinterpret_cast<const v4i*>(xs + rd_off(wm * 128 + i * 16 + fr, ck));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wf[j] = *reinterpret_cast<const v4i*>(ws + rd_off(wn * 64 + j * 16 + fr, ck));
-      if constexpr (K64) {
-        if (m & 1) wait_vm<0>();  // this wave's pieces of unit k + 1
-      } else {
-        wait_vm<4 * PP>();  // this wave's pieces of half m + 1
-      }
-      // the segment boundaries are scheduling fences: without them the compiler interleaves the
-      // fragment reads with the MFMAs and hoists most MFMAs above the barrier (into L), which
-      // undoes the ping-pong
-      __builtin_amdgcn_sched_barrier(0);
-      lds_barrier_rd();  // fragments in registers; the next unit visible to the next L
-      __builtin_amdgcn_sched_barrier(0);
-      // C_m
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(wf[j], xf[i], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-      lds_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!g1) lds_barrier();  // G1 took its extra barrier at the start: equal counts
-    wait_vm<0>();
-    lds_barrier_rd();  // every DMA landed and every fragment read done before LDS is reused
-    if (g1) __builtin_amdgcn_s_setprio(0);
-  };
-
-  v4f acc[8][4];
-  auto zero = [&]() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  };
-  if constexpr (!SK) {
-    const int bid = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
-    zero();
-    tile_loop(tmi * 256, tni * 256, 0, nu, acc);
-    nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, tmi * 256, tni * 256, tmi);
-  } else {
-    // a range spans at most two tiles (the launcher keeps per_wg <= nu): the segment that starts
-    // it and, when it crosses a tile boundary, the head of the next tile.  Two straight-line
-    // segments rather than a loop: hoisting the lane-invariant address math of the main loop and
-    // of the epilogue out of a loop kept it all live and spilled.
-    const int b = blockIdx.x;
-    const int64_t total = (int64_t)ntm * ntn * nu;
-    const int64_t it0 = (int64_t)b * S.per_wg;
-    const int64_t it1 = min(total, it0 + S.per_wg);
-    auto segment = [&](int tile, int ub, int ue) {
-      const int tmi = tile / ntn, tni = tile - (tile / ntn) * ntn;
-      zero();
-      tile_loop(tmi * 256, tni * 256, ub, ue, acc);
-      if (ub > 0) {
-        // contributor: publish the partial
-        // buffer stores: one lane offset + a scalar offset per accumulator tile (flat addresses
-        // would cost a 64-bit VGPR pair per tile: 31 KB is past the immediate-offset range)
-        const __amdgpu_buffer_rsrc_t rw = make_rsrc(S.ws, S.ws_bytes);
-        const int voff = (wid * 32 * 64 + lane) * 16;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rw, voff,
-                                                   b * 262144 + (i * 4 + j) * 1024, kCpolSc1);
-        wait_vm<0>();  // device-scope stores performed (no L2-wide writeback: buffer_wbl2 per
-        lds_barrier(); // contributor cost 3x in kernel time)
-        if (t == 0) __hip_atomic_store(S.flags + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
-      // owner: add the partials of the ranges that start inside the tile (at most kSkMaxParts), in
-      // workgroup order.  No branch around the accumulators: thread 0
-      // waits for the flags first, then every candidate is added, a missing one as zeros read
-      // through an out-of-range buffer offset (with acc modified under a branch, the compiler
-      // copied all 128 accumulators at each merge and spilled).
-      int nc = 0;
-      if (ue < nu) {
-        while (nc < kSkMaxParts && (int64_t)(b + nc + 1) * S.per_wg < (int64_t)(tile + 1) * nu) ++nc;
-        if (t == 0) {
-          for (int c = 1; c <= nc; ++c) {
-            // relaxed device-scope polls: an acquire load invalidates the XCD's whole L2 on every
-            // poll; the partials are read below with device-scope loads instead
-            while (__hip_atomic_load(S.flags + b + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-              __builtin_amdgcn_s_sleep(2);
-            __hip_atomic_store(S.flags + b + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        lds_barrier();
-      }
-      {
-        const __amdgpu_buffer_rsrc_t rw = make_rsrc(S.ws, S.ws_bytes);
-        const int lane_off = (wid * 32 * 64 + lane) * 16;
-#pragma unroll
-        for (int c = 1; c <= kSkMaxParts; ++c) {
-          const int voff = c <= nc ? lane_off : (int)OOB;
-          const int soff = (c <= nc ? b + c : 0) * 262144;
-#pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            v4f v[2][4];
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-              for (int jj = 0; jj < 4; ++jj)
-                v[ii][jj] = __builtin_bit_cast(
-                    v4f, __builtin_amdgcn_raw_buffer_load_b128(rw, voff, soff + ((i + ii) * 4 + jj) * 1024, kCpolSc1));
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-              for (int jj = 0; jj < 4; ++jj) acc[i + ii][jj] += v[ii][jj];
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-      nt_epilogue<CFG, 2, 4, 8, 4, EPI, OP_BF16>(P, acc, smem, tmi * 256, tni * 256, tmi);
-    };
-    if (it0 >= it1) return;
-    const int tile0 = (int)(it0 / nu);
-    const int ub0 = (int)(it0 - (int64_t)tile0 * nu);
-    const int ue0 = (int)min((int64_t)nu, ub0 + (it1 - it0));
-    segment(tile0, ub0, ue0);
-    if (it0 + (ue0 - ub0) < it1) {
-      lds_barrier();  // the first segment's LDS use (epilogue staging) ends before the next DMA
-      segment(tile0 + 1, 0, (int)(it1 - (int64_t)(tile0 + 1) * nu));
-    }
-  }
-}
-
-// ============================================================================
-//                      TN implicit GEMM (wgrad, split-K)
-// ============================================================================
-struct TnArgs {
-  const uint16_t* dy;  // [Mred][Kout]
-  const uint16_t* x;   // [N][H][W][C]
-  float* out;          // [splits][Kout][Ncols] (or dw directly when splits == 1)
-  uint32_t dy_bytes, x_bytes;
-  int Mred, Kout, Ncols;
-  int H, W, C, S, stride, pad, stride_w;
-  FastDiv div_hw, div_w;  // m -> n = m / (Ho*Wo), ho = rem / Wo
-  int HoWo, Wo;
-  int steps_per_split, nsteps;
-  int accumulate;      // single-split direct store: out += acc instead of out = acc
-  int staged;          // epilogue through the LDS row image (256-B segments); 0 = direct (A/B knob)
-  int Ho;
-  int adv_r, adv_qh, adv_qn;  // 64 rows = (adv_qn images, adv_qh output rows, adv_r columns)
-  int nblocks;                // > 0: grid-capped launch looping over this many logical blocks
-  float* zero;                // optional: zero_n floats workgroup 0 clears (a consumed BN-sum
-  int zero_n;                 //   accumulator, re-zeroed without a memset launch)
-};
-
-
-// RING: the stages are K32 slots (32 reduction rows of both operands) in a ring of STAGES = 4,
-// refilled three slots (1.5 K64 steps) ahead with counted vmcnt waits and one barrier per slot,
-// instead of two K64 stages with one step of lead and a vmcnt(0) drain per step -- the same LDS
-// (64 KB at BMG 128: two blocks per CU), twice the load lead.  Fragment reads are unchanged: a
-// slot is exactly one 32-row k-sub-step of the K64 image (the row swizzles repeat every 16 rows).
-template <int BMG, int BNG, int STAGES, bool RING = false>
-struct TnCfg {
-  static_assert(BNG == 128 && (BMG == 64 || BMG == 128 || BMG == 256), "TN tile shapes");
-  static_assert(RING ? STAGES == 4 : (STAGES >= 2 && STAGES <= 3), "pipeline depth");
-  static constexpr int KR = RING ? 32 : 64;           // reduction rows per stage
-  // waves: 2 x 2 (64x64 or 32x64 per wave) up to BMG = 128; 4 x 2 of 64x64 for BMG = 256, which
-  // halves the B (activation gather) loads and their per-row address math per MFMA
-  static constexpr int WAVES_M = BMG == 256 ? 4 : 2;
-  static constexpr int WAVES_N = 2;
-  static constexpr int WAVES = WAVES_M * WAVES_N;
-  static constexpr int NT = 64 * WAVES;
-  static constexpr int A_ROWB = BMG * 2;              // bytes per m row of the dy tile image
-  static constexpr int A_BYTES = KR * A_ROWB;
-  static constexpr int B_BYTES = KR * 256;            // [KR m][128 col], 256-B rows
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  // RING at BMG 256 (one 8-wave block per CU either way): room for the staged epilogue's
-  // wave-private row images too (8 waves x 64 rows x 64 fp32)
-  static constexpr int STAGED_BYTES = WAVES * (BMG / WAVES_M) * 64 * 4;
-  static constexpr int SMEM = (RING && BMG == 256 && STAGED_BYTES > STAGES * STAGE) ? STAGED_BYTES : STAGES * STAGE;
-  static constexpr int TM = BMG / WAVES_M / 16;
-  static constexpr int TN = BNG / WAVES_N / 16;
-  static constexpr int A_LPR = A_ROWB / 16;           // lanes per row in one 1-KiB DMA instruction
-  static constexpr int A_RPI = 64 / A_LPR;            // rows per instruction
-  static constexpr int A_PW = A_BYTES / 1024 / WAVES;  // DMA instructions per wave per tile
-  static constexpr int B_PW = B_BYTES / 1024 / WAVES;
-  static_assert(A_PW * 1024 * WAVES == A_BYTES && B_PW * 1024 * WAVES == B_BYTES, "tile DMA split");
-};
-
-// Main loop as igemm_nt (LDS-DMA, source-side swizzle, 2 buffers, one barrier per K-step).  One
-// DMA wave instruction moves 1 KiB = A_RPI rows of the tile; lane l fetches row
-// A_RPI*g + l/A_LPR, LDS slot l%A_LPR holding the source chunk slot ^ (swz(m)<<1).
-// Grid: 1-D over (split, tile) with split-major logical ids after the XCD remap, so the
-// column tiles of one split -- which read the same dy rows and overlapping x rows -- run on
-// the same XCD and share its L2.
-template <int BMG>
-constexpr int tn_threads() { return BMG == 256 ? 512 : 256; }  // == TnCfg<BMG, ...>::NT
-
-// PW: pointwise conv (1x1, stride 1, no padding): the x row of reduction index m IS pixel m, so a
-// B offset is m*C*2 + channel bytes -- no pixel decomposition, no bounds test (rows past the end
-// fall outside the buffer and read 0).
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING>
-__device__ __forceinline__ void tn_block(const TnArgs& P, int vb, int nblocks, char* smem) {
-  using CFG = TnCfg<BMG, BNG, STAGES, RING>;
-  constexpr int TM = CFG::TM, TN = CFG::TN, A_PW = CFG::A_PW, B_PW = CFG::B_PW;
-
-  const int ntn = (P.Ncols + BNG - 1) / BNG;
-  const int ntm = (P.Kout + BMG - 1) / BMG;
-  const int tiles = ntm * ntn;
-  const int lid = xcd_remap(vb, nblocks);
-  const int split = lid / tiles;
-  const int bid = lid - split * tiles;
-  const int tmi = bid / ntn, tni = bid - (bid / ntn) * ntn;
-  const int k0 = tmi * BMG, c0 = tni * BNG;
-  const int s_begin = split * P.steps_per_split;
-  const int s_end = min(P.nsteps, s_begin + P.steps_per_split);
-
-  const int t = threadIdx.x;
-  // uniform wave id (readfirstlane): LDS-DMA destinations become scalar math + one m0 write
-  const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
-
-  // A (dy) columns: chunk -> kout = k0 + 8*chunk ; B (x) columns: chunk -> (tap, channel).
-  // Everything per lane is precomputed.  Out-of-range columns carry a 2^31 poison in their lane
-  // offset and rows past Mred lie past the end of the buffer, so both read 0 through the buffer
-  // range check: an A load is one add.
-  int a_lane[A_PW];
-#pragma unroll
-  for (int i = 0; i < A_PW; ++i) {
-    const int arow = (wid * A_PW + i) * CFG::A_RPI + lane / CFG::A_LPR;
-    const int slot = lane % CFG::A_LPR;
-    const int chk = (swz_img<CFG::A_ROWB>(arow, slot) - arow * CFG::A_ROWB) >> 4;  // involution
-    const int acol = k0 + chk * 8;
-    a_lane[i] = acol < P.Kout ? (arow * P.Kout + acol) * 2 : (int)OOB;
-  }
-  int brow[B_PW], b_dh[B_PW], b_dw[B_PW], b_chb[B_PW];
-#pragma unroll
-  for (int i = 0; i < B_PW; ++i) {
-    brow[i] = (wid * B_PW + i) * 4 + (lane >> 4);
-    const int chk = (swz256(brow[i], lane & 15) - brow[i] * 256) >> 4;
-    const int col = c0 + chk * 8;
-    const int tap = col / P.C;
-    b_chb[i] = col < P.Ncols ? (col - tap * P.C) * 2 : (int)OOB;
-    const int r = tap / P.S;
-    b_dh[i] = r - P.pad;
-    b_dw[i] = (tap - r * P.S) - P.pad;
-  }
-  const int WC2 = P.W * P.C * 2, HWC2 = P.H * WC2, C2 = P.C * 2;
-  // general path: (n, ho, wo) of each B row, decomposed once and then advanced by 64 reduction
-  // rows per K-step with two conditional carries (issue() runs for consecutive steps) -- no
-  // quarter-rate multiply-high divisions in the loop.  Rows past Mred continue into n >= N and
-  // land past the buffer end.
-  uint32_t b_n[B_PW], b_ho[B_PW], b_wo[B_PW];
-  if constexpr (!PW) {
-#pragma unroll
-    for (int i = 0; i < B_PW; ++i) {
-      const uint32_t m = (uint32_t)(s_begin * 64 + brow[i]);
-      b_n[i] = fdiv(m, P.div_hw);
-      const uint32_t rem = m - b_n[i] * (uint32_t)P.HoWo;
-      b_ho[i] = fdiv(rem, P.div_w);
-      b_wo[i] = rem - b_ho[i] * (uint32_t)P.Wo;
-    }
-  }
-
-  auto issue = [&](int step, int buf) {
-    char* As = smem + buf * CFG::STAGE;
-    char* Bs = As + CFG::A_BYTES;
-    const int mb = step * CFG::KR;
-    const int abase = mb * P.Kout * 2;
-#pragma unroll
-    for (int i = 0; i < A_PW; ++i)
-      glds16(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
-#pragma unroll
-    for (int i = 0; i < B_PW; ++i) {
-      uint32_t off;
-      if constexpr (PW) {
-        off = (uint32_t)((mb + brow[i]) * C2 + b_chb[i]);
-      } else {
-        // 24-bit multiplies (full rate; every factor < 2^24, products < 2^32), computed
-        // unconditionally and selected: no predicated quarter-rate v_mul_lo_u32 blocks
-        const uint32_t h = __umul24(b_ho[i], (uint32_t)P.stride) + (uint32_t)b_dh[i];
-        const uint32_t w = __umul24(b_wo[i], (uint32_t)P.stride_w) + (uint32_t)b_dw[i];
-        const bool ok = h < (uint32_t)P.H && w < (uint32_t)P.W;
-        const uint32_t o = __umul24(b_n[i], (uint32_t)HWC2) + __umul24(h, (uint32_t)WC2) +
-                           __umul24(w, (uint32_t)C2) + (uint32_t)b_chb[i];
-        off = ok ? o : OOB;
-        uint32_t wo = b_wo[i] + (uint32_t)P.adv_r;
-        const uint32_t c1 = wo >= (uint32_t)P.Wo ? 1u : 0u;
-        b_wo[i] = c1 ? wo - (uint32_t)P.Wo : wo;
-        uint32_t ho = b_ho[i] + (uint32_t)P.adv_qh + c1;
-        const uint32_t c2 = ho >= (uint32_t)P.Ho ? 1u : 0u;
-        b_ho[i] = c2 ? ho - (uint32_t)P.Ho : ho;
-        b_n[i] += (uint32_t)P.adv_qn + c2;
-      }
-      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
-    }
-  };
-
-  const int wm = wid % CFG::WAVES_M, wn = wid / CFG::WAVES_M;
-  const int li = lane & 15, g = lane >> 4;  // group g covers k rows 8g..8g+7
-  // tr-read address pieces: lane 4q+p of a group -> row q, columns 4p..4p+3
-  const int tq = li >> 2, tp = li & 3;
-
-  v4f acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  // col multiple of 4; chunk = col/8, byte-in-chunk = (col%8)*2
-  auto frag_a = [&](const char* base, int row, int col) -> const char* {
-    return base + swz_img<CFG::A_ROWB>(row, col >> 3) + ((col & 7) << 1);
-  };
-  auto frag_b = [&](const char* base, int row, int col) -> const char* {
-    return base + swz256(row, col >> 3) + ((col & 7) << 1);
-  };
-
-  constexpr int LPS = A_PW + B_PW;
-  if constexpr (RING) {
-    // K32 slots j0 .. j0+nj-1; slot j lives in ring buffer j % 4.  Iteration j: wait for slot j
-    // (slots j+1, j+2 may stay in flight), barrier (RAW for slot j; WAR for buffer (j+3) % 4 =
-    // (j-1) % 4, read in iteration j-1 and retired by each wave's lgkmcnt before the barrier),
-    // then refill that buffer with slot j+3 and compute slot j.
-    const int j0 = s_begin * 2, nj = (s_end - s_begin) * 2;
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      if (p < nj) issue(j0 + p, p);
-    for (int j = 0; j < nj; ++j) {
-      wait_steps<LPS>(min(nj - 1, j + 2) - j);
-      lds_barrier_rd();
-      if (j + 3 < nj) issue(j0 + j + 3, (j + 3) & 3);
-      const char* As = smem + (j & 3) * CFG::STAGE;
-      const char* Bs = As + CFG::A_BYTES;
-      const int rowA = 8 * g + tq;
-      v4i af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        int col = wm * TM * 16 + i * 16 + 4 * tp;
-        af[i] = cat_frag(ds_read_tr(frag_a(As, rowA, col)), ds_read_tr(frag_a(As, rowA + 4, col)));
-      }
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) {
-        int col = wn * TN * 16 + jj * 16 + 4 * tp;
-        bfr[jj] = cat_frag(ds_read_tr(frag_b(Bs, rowA, col)), ds_read_tr(frag_b(Bs, rowA + 4, col)));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
-    }
-    lds_barrier_rd();  // every wave's last fragment reads retired before the staging writes
-  } else {
-  // STAGES-1 K-steps in flight ahead of the one being consumed; the buffer refilled at the top of
-  // iteration i is the one consumed in iteration i-1 (released by that iteration's barrier).
-  const int nst = s_end - s_begin;
-#pragma unroll
-  for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nst) issue(s_begin + p, p);
-  wait_steps<LPS>(min(nst, STAGES - 1) - 1);
-  lds_barrier();
-  int cur = 0, nxt = STAGES - 1;
-  for (int i = 0; i < nst; ++i) {
-    if (i + STAGES - 1 < nst) issue(s_begin + i + STAGES - 1, nxt);
-    const char* As = smem + cur * CFG::STAGE;
-    const char* Bs = As + CFG::A_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int rowA = ks * 32 + 8 * g + tq;  // m row of the first tr block
-      v4i af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        int col = wm * TM * 16 + i * 16 + 4 * tp;
-        v4s_t lo = ds_read_tr(frag_a(As, rowA, col));
-        v4s_t hi = ds_read_tr(frag_a(As, rowA + 4, col));
-        af[i] = cat_frag(lo, hi);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int col = wn * TN * 16 + j * 16 + 4 * tp;
-        v4s_t lo = ds_read_tr(frag_b(Bs, rowA, col));
-        v4s_t hi = ds_read_tr(frag_b(Bs, rowA + 4, col));
-        bfr[j] = cat_frag(lo, hi);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-    }
-    wait_steps<LPS>(min(nst - 1, i + STAGES - 1) - (i + 1));
-    lds_barrier();
-    cur = cur + 1 == STAGES ? 0 : cur + 1;
-    nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
-  }
-  }  // !RING
-
-  // epilogue: lane holds rows fq*4+e, column fr.  ATOMIC: fp32 atomic add into the zeroed dW
-  // (16 lanes = 64 contiguous bytes per row; split count bounded so atomic bytes stay small);
-  // otherwise a private fp32 [Kout][Ncols] slab per split, summed by splitk_reduce_kernel.
-  const int fq = lane >> 4, fr = lane & 15;
-  float* o = ATOMIC ? P.out : P.out + (int64_t)split * P.Kout * P.Ncols;
-  // Staged form: the 16x16 accumulator layout gives every store / atomic wave-instruction four
-  // 64-B row pieces; through a wave-private row-major LDS image (the drained pipeline buffers:
-  // every DMA landed and every wave passed the loop's last barrier) each instruction instead
-  // covers one 256-B segment of a dW row, the shape float atomics run at full rate
-  // (MI355X_MICROARCH "Global float atomics").  Column XOR 16 on rows 4..7 mod 8 keeps both the
-  // fragment writes (lanes fq=0/1 are 4 rows apart) and the row reads conflict-free.
-  constexpr bool STAGED = TN * 16 == 64 && CFG::WAVES * TM * 16 * 64 * 4 <= CFG::SMEM;
-  if (STAGED && P.staged) {
-    float* stg = reinterpret_cast<float*>(smem) + wid * (TM * 16) * 64;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = i * 16 + fq * 4 + e;
-          stg[r * 64 + ((j * 16 + fr) ^ (((r >> 2) & 1) << 4))] = acc[i][j][e];
-        }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the region is wave-private
-    __builtin_amdgcn_wave_barrier();
-    const int col = c0 + wn * 64 + lane;
-    const int row0 = k0 + wm * TM * 16;
-    if (col < P.Ncols) {
-#pragma unroll 8
-      for (int r = 0; r < TM * 16; ++r) {
-        const float v = stg[r * 64 + (lane ^ (((r >> 2) & 1) << 4))];
-        if (row0 + r < P.Kout) {
-          float* dst = o + (int64_t)(row0 + r) * P.Ncols + col;
-          if (ATOMIC) unsafeAtomicAdd(dst, v);
-          else if (P.accumulate) *dst += v;
-          else *dst = v;
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      int col = c0 + wn * TN * 16 + j * 16 + fr;
-      if (col >= P.Ncols) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        int row = k0 + wm * TM * 16 + i * 16 + fq * 4 + e;
-        if (row < P.Kout) {
-          if (ATOMIC) unsafeAtomicAdd(o + (int64_t)row * P.Ncols + col, acc[i][j][e]);
-          else if (P.accumulate) o[(int64_t)row * P.Ncols + col] += acc[i][j][e];
-          else o[(int64_t)row * P.Ncols + col] = acc[i][j][e];
-        }
-      }
-    }
-}
-
-// Grid-capped launch (TnArgs::nblocks > 0, PDT_TN_GRID_CAP): gridDim.x workgroups loop over the
-// nblocks logical blocks, so the weight-gradient stream never holds more than the cap's share of
-// the CUs while the dgrad chain runs beside it.  Measured (r4u, ResNet-50 b256): no cap 19.06 ms,
-// cap 256 19.37, 512 19.07, 768 19.06; --force-comm 19.60 with and without cap 512 -- it does not
-// replace the main-stream priority, so it stays an A/B knob (profiles/r4u_tn_grid_cap_ab.jsonl).
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW, bool RING = false>
-__global__ void __launch_bounds__(tn_threads<BMG>()) igemm_tn_kernel(const TnArgs P) {
-  static_assert(TnCfg<BMG, BNG, STAGES, RING>::NT == tn_threads<BMG>(), "launch bounds");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (P.zero != nullptr && blockIdx.x == 0)  // ordered after the accumulator's consumer by the caller
-    for (int i = threadIdx.x; i < P.zero_n; i += blockDim.x) P.zero[i] = 0.f;
-  if (P.nblocks <= 0) {
-    tn_block<BMG, BNG, STAGES, ATOMIC, PW, RING>(P, blockIdx.x, gridDim.x, smem);
-    return;
-  }
-  for (int vb = blockIdx.x; vb < P.nblocks; vb += gridDim.x) {
-    tn_block<BMG, BNG, STAGES, ATOMIC, PW, RING>(P, vb, P.nblocks, smem);
-    __syncthreads();  // the epilogue's LDS staging is read before the next block's DMA lands
-  }
 }
 
 // ============================================================================
@@ -2167,30 +1480,6 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
   }
 }
 
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits,
-                                                            int64_t n, float* __restrict__ out,
-                                                            int accumulate) {
-  int64_t n4 = n / 4;
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 s = reinterpret_cast<const float4*>(ws)[i];
-    for (int k = 1; k < splits; ++k) {
-      float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n)[i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    if (accumulate) {
-      float4 o = reinterpret_cast<float4*>(out)[i];
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-    }
-    reinterpret_cast<float4*>(out)[i] = s;
-  }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(int64_t)k * n + i];
-    out[i] = accumulate ? out[i] + s : s;
-  }
-}
-
 // ============================================================================
 //                                   host side
 // ============================================================================
@@ -2219,29 +1508,16 @@ static void run_nt(const NtArgs& a, hipStream_t st) {
   check_launch("igemm_nt");
 }
 
-// The quadrant-phased 256x256 kernel (igemm_ntq_kernel) replaces the 2-stage 256x256 NT tile for
-// C64 bf16 launches.  PDT_NTQ=0 restores the old tile (A/B knob).
-// PDT_NTQ: bit 0 = the bf16 256x256 tile, bit 1 = the bf16 128x128 tile, bit 2 = the fp8 256x256
-// tile, bit 3 = the read-ahead (PIPE) loop for the bf16 256x256 tile, bit 4 / bit 5 = the
-// ping-pong 256x256 kernel (igemm_ntp_kernel) with the K32 ring / K64 stages (win over bits 0 / 3) (default 3 = the quadrant-phased kernel on both; 33 = ping-pong K64; 0 = none)
-static int ntq_mode() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_NTQ");
-    // default 3: the quadrant-phased kernel on the 256x256 AND the 128x128 bf16 tiles (r4ab,
-    // interleaved: 18.86 / 18.85 ms vs 18.93 / 18.92 / 18.97 with 1).  The ping-pong K64 kernel
-    // (33) wins the isolated GEMMs (r4h: 4096^3 1303 vs 1272 TF, 50176x2304 922 vs 899) but loses
-    // ~0.1 ms in the ResNet-50 step (r4h 18.94 vs 18.81 ms, r4z 19.19 vs 19.11 ms)
-    v = e ? atoi(e) : 3;
-  }
-  return v;
-}
-
-template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16, bool PIPE = false>
+// The quadrant-phased kernel (igemm_ntq_kernel) runs the bf16 256x256 and 128x128 C64 tiles (r4ab,
+// interleaved: 18.86 / 18.85 ms vs 18.93 / 18.92 / 18.97 on the 256x256 tile alone).  Measured and
+// removed in round 5 (git history: 242a23b): the ping-pong 256x256 kernel (won isolated GEMMs, lost
+// ~0.1 ms in the step), the read-ahead NTQ loop, stream-K for sub-wave grids (owners spun beside
+// the side-stream wgrads: 40 vs 19 ms/step) and the fp8 quadrant-phased tile.
+template <int WM, int WN, int TMQ, int TNQ, int EPI, int OP = OP_BF16>
 static void run_ntq(const NtArgs& a, hipStream_t st) {
   using Q = NtqCfg<WM, WN, TMQ, TNQ>;
   const int ntm = (a.M + Q::BM - 1) / Q::BM, ntn = (a.Nout + Q::BN - 1) / Q::BN;
-  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI, OP, PIPE>;
+  auto kfn = igemm_ntq_kernel<WM, WN, TMQ, TNQ, EPI, OP>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, Q::SMEM);
@@ -2249,133 +1525,6 @@ static void run_ntq(const NtArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(Q::NT), Q::SMEM, st, a);
   check_launch("igemm_ntq");
-}
-
-template <int EPI, bool K64>
-static void run_ntp(const NtArgs& a, hipStream_t st) {
-  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
-  auto kfn = igemm_ntp_kernel<EPI, K64, false>;
-  constexpr int smem = 4 * 32768;  // 2 K64 stages / 4 K32 slots (= the epilogue's staging)
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kfn, dim3(ntm * ntn), dim3(512), smem, st, a, NtpSk{nullptr, nullptr, 0, 0});
-  check_launch("igemm_ntp");
-}
-
-// Stream-K workspace: one 256 KB fp32 slot and one flag per workgroup, per (device, stream) --
-// two streams never share flags, so concurrent stream-K GEMMs cannot consume each other's
-// partials.  Flags start at zero and every owner resets the ones it consumed.  Allocated on the
-// first eager launch; a launch under graph capture with no workspace yet falls back to the
-// plain kernel.
-struct SkWorkspace {
-  float* ws = nullptr;
-  uint32_t* flags = nullptr;
-  int slots = 0;
-};
-static SkWorkspace* sk_workspace(hipStream_t st, int slots) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, SkWorkspace> all;
-  int dev = 0;
-  hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lock(mu);
-  SkWorkspace& s = all[{dev, st}];
-  if (s.slots >= slots) return &s;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
-  auto ck = [](hipError_t e) {
-    if (e != hipSuccess) throw std::runtime_error(std::string("stream-K workspace: ") + hipGetErrorString(e));
-  };
-  if (s.ws) {
-    ck(hipStreamSynchronize(st));
-    ck(hipFree(s.ws));
-    ck(hipFree(s.flags));
-  }
-  ck(hipMalloc(&s.ws, (size_t)slots * 65536 * sizeof(float)));
-  ck(hipMalloc(&s.flags, (size_t)slots * sizeof(uint32_t)));
-  ck(hipMemsetAsync(s.flags, 0, (size_t)slots * sizeof(uint32_t), st));
-  s.slots = slots;
-  return &s;
-}
-
-static int device_cus() {
-  static int cus[16] = {0};
-  int dev = 0;
-  hipGetDevice(&dev);
-  if (!cus[dev & 15]) {
-    int v = 0;
-    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-    cus[dev & 15] = v > 0 ? v : 256;
-  }
-  return cus[dev & 15];
-}
-
-// PDT_NT_SK: 0 = off (default), 1 = stream-K for 256x256-tile grids smaller than the CU count,
-// 2 = force it wherever the 256x256 tile could run (tests).  Measured slower (r4n, one MI355X):
-// 50176x2304->256 672 vs 893 TF isolated (partials cross XCDs through HBM: 256 KB per split tile
-// each way, plus the spilled reduction block), and the ResNet-50 step 40.0 vs 18.9 ms -- owners
-// spin on CUs while the side-stream wgrad kernels hold the CUs their contributors need.
-static int nt_sk_mode() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_NT_SK");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-// units of 64 channels per 256x256 tile, and whether stream-K applies to this launch
-// GEMM dimensions for which stream-K runs (kg_bytes = B-row bytes: nu = kg_bytes / 128 K64 units).
-// conv_nt_group_rows returns 256 for these too, so the BN partial row groups match the 256-row
-// tiles whichever 256-row kernel ends up running (the stream-K kernel needs CA % 64 == 0 and no
-// halo staging; otherwise the plain 256x256 tile runs)
-static bool sk_dims(int M, int Nout, int kg_bytes) {
-  const int mode = nt_sk_mode();
-  if (mode == 0 || Nout < 128 || kg_bytes % 128 != 0) return false;
-  const int64_t tiles = (int64_t)((M + 255) / 256) * ((Nout + 255) / 256);
-  const int nu = kg_bytes / 128;
-  if (mode == 2) return nu >= 2;
-  return tiles < device_cus() && nu >= 8 && tiles * nu >= 2 * device_cus();
-}
-
-static bool use_stream_k(const NtArgs& a) {
-  // (a dgrad parity class may hold fewer taps than the B row: nu counts this launch's taps)
-  return a.CA % 64 == 0 && a.halo_rows == 0 && a.M > 0 && a.ntaps * (a.CA / 64) >= 2 &&
-         sk_dims(a.M, a.Nout, a.Kg * 2);
-}
-
-static std::atomic<int64_t> g_sk_launches{0};
-int64_t conv_stream_k_launches() { return g_sk_launches.load(); }
-
-template <int EPI>
-static void run_ntp_sk(const NtArgs& a, hipStream_t st) {
-  const int ntm = (a.M + 255) / 256, ntn = (a.Nout + 255) / 256;
-  const int nu = a.ntaps * (a.CA / 64);
-  const int64_t total = (int64_t)ntm * ntn * nu;
-  const int cus = device_cus();
-  // per_wg <= nu: a range spans at most two tiles (the kernel runs two straight-line segments);
-  // nu / kSkMaxParts <= per_wg <= nu: at most kSkMaxParts partials per tile
-  const int per_wg = (int)std::max<int64_t>(std::min<int64_t>((total + cus - 1) / cus, nu),
-                                            (nu + kSkMaxParts - 1) / kSkMaxParts);
-  const int grid = (int)((total + per_wg - 1) / per_wg);
-  SkWorkspace* w = sk_workspace(st, cus);
-  if (w == nullptr) {  // first use under graph capture: no allocation possible
-    run_ntp<EPI, true>(a, st);
-    return;
-  }
-  auto kfn = igemm_ntp_kernel<EPI, true, true>;
-  constexpr int smem = 4 * 32768;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), smem, st, a,
-                     NtpSk{w->ws, w->flags, per_wg, (uint32_t)((size_t)cus * 65536 * sizeof(float))});
-  check_launch("igemm_ntp_sk");
-  g_sk_launches.fetch_add(1);
 }
 
 template <int WM, int WN, int TM, int TN, int EPI>
@@ -2396,22 +1545,13 @@ static void run_nt_halo(const NtArgs& a, hipStream_t st) {
 
 // Halo staging for 3x3 / stride 1 / pad 1 convolutions (fwd and dgrad): fills the halo fields of
 // `a` for the tile the dispatcher will pick and returns false where it does not apply or does
-// not fit in LDS.  PDT_HALO=0 disables it (A/B knob).
-static bool halo_mode() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_HALO");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
+// not fit in LDS.
 static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
   // Measured on MI355X (r2p/r2q, bench_conv.py, batch 256): halo staging pays where one channel
   // block covers the whole reduction (C = 64, ResNet layer1: fwd 114 -> 103 us, dgrad 111 -> 98,
   // BN-fused dgrad 140 -> 130); with several channel blocks the halo reload per block stalls
   // (128x28x28: 86 -> 93 us, 512x7x7: 75 -> 88), so those keep the per-tap A tiles.
-  if (!halo_mode() || R != 3 || S != 3 || tap_stride != 1 || pad != 1 || a.CA != 64 || !a.dense) return false;
+  if (R != 3 || S != 3 || tap_stride != 1 || pad != 1 || a.CA != 64 || !a.dense) return false;
   int bm = 0, bn = 0;
   conv_nt_tile(a.M, a.Nout, a.Kg * 2, &bm, &bn);
   const int WP = a.WA + 2;
@@ -2435,26 +1575,8 @@ static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
 // deeper prefetch pay on the huge-M, short-K layer1 GEMMs -- forward 64->256 1x1 136 -> 120 us,
 // 256->64 117 -> 103, and the 64-channel dgrads -- while every long-K conv loses 5-20% to the
 // doubled barriers and fragment-read restarts (256x14x14 3x3 68 -> 79 us).  Policy: K32 for
-// M >= 786432 on forward (stats epilogue) GEMMs and 64-column dgrads.  PDT_NT_K32=0/1 forces one
-// mode for every tile ("a,b,c,d" per tile: 256x64, 64x128, 256x256, 128x128).
-static int nt_k32_env(int which) {
-  static int v[4] = {-2, -2, -2, -2};
-  if (v[0] == -2) {
-    v[0] = v[1] = v[2] = v[3] = -1;  // -1: policy
-    if (const char* e = getenv("PDT_NT_K32")) {
-      int x[4];
-      if (sscanf(e, "%d,%d,%d,%d", &x[0], &x[1], &x[2], &x[3]) == 4)
-        for (int k = 0; k < 4; ++k) v[k] = x[k] ? 1 : 0;
-      else
-        v[0] = v[1] = v[2] = v[3] = atoi(e) ? 1 : 0;
-    }
-  }
-  return v[which];
-}
-
-static bool nt_k32(int which, const NtArgs& a, int epi) {
-  const int e = nt_k32_env(which);
-  if (e >= 0) return e == 1;
+// M >= 786432 on forward (stats epilogue) GEMMs and 64-column dgrads.
+static bool nt_k32(const NtArgs& a, int epi) {
   return a.M >= 786432 && (epi == EPI_STATS || a.Nout <= 64);
 }
 
@@ -2463,44 +1585,23 @@ static bool nt_k32(int which, const NtArgs& a, int epi) {
 // DMA issues and cuts fragment reads by a quarter per MFMA, but runs one block per CU, so it only
 // pays with enough blocks (>= 196, measured on the ResNet-50 shape classes: +10-20% on the 28x28
 // and 14x14 layers, -40% on 7x7 with 98 blocks) and a K loop longer than one step.
-// PDT_NT_TILE=1 disables it, =2 forces it wherever Nout >= 256 (tuning knob).
-static int nt_tile_mode() {
-  static int v = -1;
-  if (v < 0) {
-    v = 0;
-    if (const char* e = getenv("PDT_NT_TILE")) v = atoi(e);
-  }
-  return v;
-}
-
 static bool use_wide_tile(int M, int Nout, int kg_bytes) {
-  const int mode = nt_tile_mode();
-  if (mode == 1 || Nout < 256) return false;
-  if (mode == 2) return true;
+  if (Nout < 256) return false;
   const int64_t blocks = (int64_t)((M + 255) / 256) * ((Nout + 255) / 256);
   return kg_bytes >= 256 && blocks >= 196;
 }
 
-// Short-K GEMMs with Nout % 256 == 0 (the 1x1 convs' K <= PDT_NT_MID elements): a 4-wave 128x256
+// Short-K GEMMs with Nout % 256 == 0 (the 1x1 convs' K <= 512 elements): a 4-wave 128x256
 // tile (waves of 64x128, the 256x256 tile's wave shape) on the K32 ring, so its LDS (72 KB) lets
 // TWO blocks share a CU: one block's epilogue stores overlap the other's loads and MFMAs.  The
 // 8-wave 256x256 tile holds a CU alone, and its phases (load, MFMA, store) run back to back:
 // PDT_NT_TIMING measured ~45 % of a 256x256 short-K tile in the store phase while HBM idles in
 // the load/MFMA phases.  Measured on MI355X (r3j, one box, batch 256): ResNet-50 step 19.24 ms
 // (off) -> 18.94 (K <= 512) / 18.95 (K <= 256) / 19.06 (K <= 1024); isolated fwd 4.22 -> 4.16 ms,
-// BN-fused dgrad 5.65 -> 5.52 ms.  0 disables it.
-static int nt_mid_kmax() {
-  static int v = -1;
-  if (v < 0) {
-    v = 512;
-    if (const char* e = getenv("PDT_NT_MID")) v = std::max(0, atoi(e));
-  }
-  return v;
-}
-
+// BN-fused dgrad 5.65 -> 5.52 ms.
 static bool use_mid_tile(int M, int Nout, int kg_bytes) {
-  const int kmax = nt_mid_kmax();
-  return kmax > 0 && M > 8192 && Nout % 256 == 0 && kg_bytes <= 2 * kmax;
+  constexpr int kmax = 512;
+  return M > 8192 && Nout % 256 == 0 && kg_bytes <= 2 * kmax;
 }
 
 // Tile choice: output channels 64 -> tall 256x64 tile (more M rows per block); small M -> short
@@ -2510,7 +1611,6 @@ static bool use_mid_tile(int M, int Nout, int kg_bytes) {
 // size those buffers with it, dispatch_nt picks its tile with it -- one definition for both.
 int conv_nt_group_rows(int M, int Nout, int kg_bytes) {
   if (Nout <= 64) return 256;
-  if (sk_dims(M, Nout, kg_bytes)) return 256;  // stream-K (sub-wave grids of long-K 256x256 tiles)
   // small M takes the short 64x128 tile (enough blocks) -- unless the 256x256 grid alone fills the
   // chip: a 4096^3 GEMM (M = 4096) ran the 64x128 tile at 642 TF/s (VERDICT r3 weak #2 measured
   // that tile, not the 256x256 one)
@@ -2543,12 +1643,6 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     }
   }
   if constexpr (OP != OP_BF16) {  // fp8: 2-stage pipeline only (fewer instantiations)
-    if constexpr (C64) {
-      if (rows == 256 && a.Nout > 64 && (ntq_mode() & 4)) {  // PDT_NTQ bit 2: quadrant-phased fp8 256x256
-        run_ntq<2, 4, 4, 2, EPI, OP>(a, st);
-        return;
-      }
-    }
     if (a.Nout <= 64) run_nt<4, 1, 4, 4, 2, C64, EPI, OP>(a, st);
     else if (rows == 64) run_nt<2, 2, 2, 4, 2, C64, EPI, OP>(a, st);
     else if (rows == 256) run_nt<4, 2, 4, 8, 2, C64, EPI, OP>(a, st);
@@ -2556,39 +1650,29 @@ static void dispatch_nt(const NtArgs& a, hipStream_t st) {
     return;
   }
   if constexpr (C64 && OP == OP_BF16) {
-    if (use_stream_k(a)) {
-      run_ntp_sk<EPI>(a, st);
+    if (rows == 256 && a.Nout > 64) {  // (Nout <= 64 is the 256x64 tile)
+      run_ntq<2, 4, 4, 2, EPI>(a, st);
       return;
     }
-    if (rows == 256 && a.Nout > 64 && (ntq_mode() & 48)) {  // ping-pong wave groups
-      if (ntq_mode() & 32) run_ntp<EPI, true>(a, st);  // K64 stages
-      else run_ntp<EPI, false>(a, st);                 // K32 ring
-      return;
-    }
-    if (rows == 256 && a.Nout > 64 && (ntq_mode() & 1)) {  // (Nout <= 64 is the 256x64 tile)
-      if (ntq_mode() & 8) run_ntq<2, 4, 4, 2, EPI, OP_BF16, true>(a, st);
-      else run_ntq<2, 4, 4, 2, EPI>(a, st);
-      return;
-    }
-    if (rows == 128 && (ntq_mode() & 2) && a.Nout > 64 && !use_mid_tile(a.M, a.Nout, a.Kg * 2)) {
+    if (rows == 128 && a.Nout > 64 && !use_mid_tile(a.M, a.Nout, a.Kg * 2)) {
       run_ntq<2, 2, 2, 2, EPI>(a, st);
       return;
     }
   }
   const bool k32ok = C64 || !a.c8;  // the 8-channel (stem) loader packs 8 taps per K64 step
   if (a.Nout <= 64) {
-    if (k32ok && nt_k32(0, a, EPI)) run_nt<4, 1, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 256 x 64
+    if (k32ok && nt_k32(a, EPI)) run_nt<4, 1, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 256 x 64
     else run_nt<4, 1, 4, 4, 2, C64, EPI>(a, st);
   } else if (rows == 64) {
-    if (k32ok && nt_k32(1, a, EPI)) run_nt<2, 2, 2, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 64 x 128
+    if (k32ok && nt_k32(a, EPI)) run_nt<2, 2, 2, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 64 x 128
     else run_nt<2, 2, 2, 4, 2, C64, EPI>(a, st);
   } else if (rows == 256) {
-    if (k32ok && nt_k32(2, a, EPI)) run_nt<4, 2, 4, 8, 5, C64, EPI, OP_BF16, true>(a, st);  // 256 x 256
+    if (k32ok && nt_k32(a, EPI)) run_nt<4, 2, 4, 8, 5, C64, EPI, OP_BF16, true>(a, st);  // 256 x 256
     else run_nt<4, 2, 4, 8, 2, C64, EPI>(a, st);
   } else if (k32ok && use_mid_tile(a.M, a.Nout, a.Kg * 2)) {
     run_nt<2, 2, 4, 8, 3, C64, EPI, OP_BF16, true>(a, st);  // 128 x 256, K32 ring, 2 blocks / CU
   } else {
-    if (k32ok && nt_k32(3, a, EPI)) run_nt<2, 2, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 128 x 128
+    if (k32ok && nt_k32(a, EPI)) run_nt<2, 2, 4, 4, 4, C64, EPI, OP_BF16, true>(a, st);  // 128 x 128
     else run_nt<2, 2, 4, 4, 2, C64, EPI>(a, st);
   }
 }
@@ -2756,130 +1840,7 @@ void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* os
   conv_dgrad_impl<OP_F8_E5M2>(dy, wt, oscale, ascale, dx, addend, s, st, bn, addend_sub);
 }
 
-// ------------------------------------------------------------------- wgrad
-// Pipeline depth per TN tile width; PDT_TN_STAGES="<bmg64>,<bmg128>" overrides (tuning knob).
-static int tn_stages(int bmg) {
-  static int st64 = -1, st128 = -1;
-  if (st64 < 0) {
-    st64 = 2; st128 = 2;
-    if (const char* e = getenv("PDT_TN_STAGES")) {
-      int a = 0, b = 0;
-      if (sscanf(e, "%d,%d", &a, &b) == 2) { st64 = a == 3 ? 3 : 2; st128 = b == 3 ? 3 : 2; }
-    }
-  }
-  return bmg == 64 ? st64 : st128;
-}
-
-// K32-slot ring for the TN tiles (TnCfg RING), PDT_TN_RING=1.  Off by default: measured slower
-// on MI355X (r4b, bench_conv.py, same call): ResNet-50 wgrad total 5.77 ms with the ring vs 4.74
-// ms with the two-stage K64 loop -- a barrier (and lgkmcnt drain) per 16 MFMAs per wave costs
-// more than the deeper load lead gains.
-static bool tn_ring() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_TN_RING");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
-struct WgradPlan {
-  int bmg, bng, tiles, splits, steps_per_split, nsteps;
-};
-
-static WgradPlan plan_wgrad(const ConvShape& s, bool deterministic) {
-  WgradPlan p;
-  // PDT_TN_WIDE=1: 8-wave 256x128 tile when Kout % 256 == 0.  It halves the activation-gather
-  // loads and their address math per MFMA, but measured 5-20% SLOWER on every ResNet-50 wgrad
-  // shape (one 96-KB block per CU hides less latency than two 4-wave 48-KB blocks), so it is off.
-  static int wide = -1;
-  if (wide < 0) {
-    const char* e = getenv("PDT_TN_WIDE");
-    wide = (e && e[0] == '1') ? 1 : 0;
-  }
-  p.bmg = s.K <= 64 ? 64 : ((wide && s.K % 256 == 0) ? 256 : 128);
-  p.bng = 128;
-  const int ncols = s.R * s.S * s.C;
-  p.tiles = ((s.K + p.bmg - 1) / p.bmg) * ((ncols + p.bng - 1) / p.bng);
-  const int64_t mred = (int64_t)s.N * s.Ho * s.Wo;
-  p.nsteps = (int)((mred + 63) / 64);
-  int target = p.bmg == 256 ? 512 : (p.tiles <= 4 ? 2048 : 1024);  // ~4 4-wave (2 8-wave) blocks per CU
-  int splits = (target + p.tiles - 1) / p.tiles;
-  splits = std::min(splits, std::max(1, p.nsteps / 8));  // >= 8 K-steps per split
-  // bound the reduction traffic: atomics/slabs move splits * |dW| * 4 bytes
-  const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
-  // PDT_WGRAD_CAP_MB="<atomic>,<slab>" overrides the reduction-traffic caps (tuning knob)
-  static int64_t cap_atomic = -1, cap_slab = -1;
-  if (cap_atomic < 0) {
-    // slab cap 32 MB (was 64): deterministic ResNet-50 step 19.21 ms vs 20.08 at 64, 19.28 at 24,
-    // 19.72 at 16, 22.16 at 8; non-deterministic 19.01 in the same call (r4x / r4y)
-    cap_atomic = 32; cap_slab = 32;
-    if (const char* e = getenv("PDT_WGRAD_CAP_MB")) {
-      int a = 0, b = 0;
-      if (sscanf(e, "%d,%d", &a, &b) == 2 && a > 0 && b > 0) { cap_atomic = a; cap_slab = b; }
-    }
-  }
-  const int64_t cap_bytes = (deterministic ? cap_slab : cap_atomic) << 20;
-  splits = std::min<int64_t>(splits, std::max<int64_t>(1, cap_bytes / dw_bytes));
-  // atomic split-K: up to 1024 slices (the stem's 2-tile, 50k-step wgrad runs last in backward,
-  // on the critical path: 256 slices left it at 2 blocks per CU); slabs keep 256
-  splits = std::max(1, std::min(splits, deterministic ? 256 : 1024));
-  p.steps_per_split = (p.nsteps + splits - 1) / splits;
-  p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
-  return p;
-}
-
-void conv_wgrad_plan_v2(const ConvShape& s, bool deterministic, int out[4]);
-size_t conv_wgrad_ws_floats_v2(const ConvShape& s, bool deterministic);
-void launch_conv_wgrad_v2(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                          const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
-                          float* zero, int zero_n);
-static bool wg_v1() {  // PDT_WG_V1=1: the round-4 TN kernel (A/B only)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("PDT_WG_V1"); v = (e && e[0] == '1') ? 1 : 0; }
-  return v == 1;
-}
-
-void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]) {
-  if (!wg_v1()) return conv_wgrad_plan_v2(s, deterministic, out);
-  const WgradPlan p = plan_wgrad(s, deterministic);
-  out[0] = p.bmg; out[1] = p.bng; out[2] = p.tiles; out[3] = p.splits;
-}
-
-size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
-  if (!wg_v1()) return conv_wgrad_ws_floats_v2(s, deterministic);
-  if (!deterministic) return 0;
-  WgradPlan p = plan_wgrad(s, true);
-  if (p.splits <= 1) return 0;
-  return (size_t)p.splits * s.K * s.R * s.S * s.C;
-}
-
-template <int BMG, int BNG, int STAGES, bool ATOMIC, bool PW = false, bool RING = false>
-static void run_tn(const TnArgs& a, int tiles, int splits, hipStream_t st) {
-  using CFG = TnCfg<BMG, BNG, STAGES, RING>;
-  auto kfn = igemm_tn_kernel<BMG, BNG, STAGES, ATOMIC, PW, RING>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, CFG::SMEM);
-    attr_set = true;
-  }
-  // PDT_TN_GRID_CAP=<n>: at most n workgroups, looping over the tiles x splits blocks (A/B knob)
-  static int cap = -1;
-  if (cap < 0) {
-    const char* e = getenv("PDT_TN_GRID_CAP");
-    cap = e ? std::max(0, atoi(e)) : 0;
-  }
-  const int nb = tiles * splits;
-  if (cap > 0 && nb > cap) {
-    TnArgs b = a;
-    b.nblocks = nb;
-    hipLaunchKernelGGL(kfn, dim3(cap), dim3(CFG::NT), CFG::SMEM, st, b);
-  } else {
-    hipLaunchKernelGGL(kfn, dim3(nb), dim3(CFG::NT), CFG::SMEM, st, a);
-  }
-  check_launch("igemm_tn");
-}
-
+// ------------------------------------------------------------------- wgrad (bf16: wgrad.hip)
 // fp8 weight gradient (igemm_tn_f8_kernel): split-K planned like plan_wgrad with 128-pixel steps
 void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]) {
   const int bmg = s.K % 128 == 0 ? 128 : 64;
@@ -2935,78 +1896,6 @@ void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* d
     else hipLaunchKernelGGL((igemm_tn_f8_kernel<64, false>), dim3(grid), dim3(256), smem, st, a);
   }
   check_launch("igemm_tn_f8");
-}
-
-void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
-                       const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
-                       float* zero, int zero_n) {
-  if (!wg_v1()) return launch_conv_wgrad_v2(dy, x, dw, ws, s, deterministic, accumulate, st, zero, zero_n);
-  if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
-  WgradPlan p = plan_wgrad(s, deterministic);
-  const bool slab = deterministic && p.splits > 1;
-  const bool atomic = !deterministic && p.splits > 1;
-  TnArgs a{};
-  a.dy = dy; a.x = x;
-  a.out = slab ? ws : dw;
-  a.dy_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
-  a.x_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
-  a.Mred = s.N * s.Ho * s.Wo; a.Kout = s.K; a.Ncols = s.R * s.S * s.C;
-  a.H = s.H; a.W = s.W; a.C = s.C; a.S = s.S; a.stride = s.stride; a.pad = s.pad; a.stride_w = s.sw();
-  a.HoWo = s.Ho * s.Wo; a.Wo = s.Wo;
-  a.div_hw = make_fastdiv((uint32_t)a.HoWo);
-  a.div_w = make_fastdiv((uint32_t)s.Wo);
-  a.steps_per_split = p.steps_per_split;
-  a.nsteps = p.nsteps;
-  a.accumulate = (accumulate && !slab) ? 1 : 0;  // slabs are private partials: always overwritten
-  a.zero = zero_n > 0 ? zero : nullptr;
-  a.zero_n = zero_n;
-  static int staged = -1;
-  if (staged < 0) {
-    const char* e = getenv("PDT_TN_STAGED");
-    staged = (e && e[0] == '0') ? 0 : 1;
-  }
-  a.staged = staged;
-  const int64_t n = (int64_t)s.K * a.Ncols;
-  if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
-  const bool deep = p.bmg == 64 ? tn_stages(64) == 3 : tn_stages(128) == 3;
-  const bool ring = tn_ring() && !deep;
-  const int kr = ring ? 32 : 64;  // reduction rows per pipeline stage
-  a.Ho = s.Ho;
-  a.adv_r = kr % s.Wo;
-  a.adv_qh = (kr / s.Wo) % s.Ho;
-  a.adv_qn = (kr / s.Wo) / s.Ho;
-  const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 &&
-                  s.H == s.Ho && s.W == s.Wo;
-  if (ring) {
-    if (p.bmg == 256) {  // PDT_TN_WIDE=1: 8-wave 256x128 tile, one block per CU
-      if (pw) { if (atomic) run_tn<256, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<256, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
-      else { if (atomic) run_tn<256, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<256, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
-    } else if (p.bmg == 64) {
-      if (pw) { if (atomic) run_tn<64, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
-      else { if (atomic) run_tn<64, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
-    } else {
-      if (pw) { if (atomic) run_tn<128, 128, 4, true, true, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 4, false, true, true>(a, p.tiles, p.splits, st); }
-      else { if (atomic) run_tn<128, 128, 4, true, false, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 4, false, false, true>(a, p.tiles, p.splits, st); }
-    }
-  } else if (pw && !deep && p.bmg != 256) {
-    if (p.bmg == 64) { if (atomic) run_tn<64, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false, true>(a, p.tiles, p.splits, st); }
-    else { if (atomic) run_tn<128, 128, 2, true, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 2, false, true>(a, p.tiles, p.splits, st); }
-  } else if (p.bmg == 256) {
-    if (atomic) run_tn<256, 128, 2, true>(a, p.tiles, p.splits, st);
-    else run_tn<256, 128, 2, false>(a, p.tiles, p.splits, st);
-  } else if (p.bmg == 64) {
-    if (deep) { if (atomic) run_tn<64, 128, 3, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 3, false>(a, p.tiles, p.splits, st); }
-    else { if (atomic) run_tn<64, 128, 2, true>(a, p.tiles, p.splits, st); else run_tn<64, 128, 2, false>(a, p.tiles, p.splits, st); }
-  } else {
-    if (deep) { if (atomic) run_tn<128, 128, 3, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 3, false>(a, p.tiles, p.splits, st); }
-    else { if (atomic) run_tn<128, 128, 2, true>(a, p.tiles, p.splits, st); else run_tn<128, 128, 2, false>(a, p.tiles, p.splits, st); }
-  }
-  if (slab) {
-    int64_t b = (n / 4 + 255) / 256;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 4096))),
-                       dim3(256), 0, st, ws, p.splits, n, dw, accumulate ? 1 : 0);
-    check_launch("splitk_reduce");
-  }
 }
 
 }  // namespace pdt

@@ -68,7 +68,6 @@ int conv_nt_group_rows(int M, int Nout, int kg_bytes);
 // (BM, BN) of the NT workgroup tile the fwd / dgrad launch of such a GEMM runs (test introspection)
 void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn);
 // number of stream-K NT launches so far in this process (tests: which path ran)
-int64_t conv_stream_k_launches();
 // PDT_NT_TIMING builds (scripts/build_variant.sh): per-workgroup phase timestamps of NT launches
 // (s_memtime at start / first operands in LDS / main loop done / epilogue stats done / end, plus
 // s_memrealtime and the CU id), 8 values per block id, copied into `host`; other builds return 0.

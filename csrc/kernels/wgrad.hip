@@ -701,12 +701,12 @@ static WgPlan plan_wg(const ConvShape& s, bool deterministic) {
   return p;
 }
 
-void conv_wgrad_plan_v2(const ConvShape& s, bool deterministic, int out[4]) {
+void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]) {
   const WgPlan p = plan_wg(s, deterministic);
   out[0] = p.bm; out[1] = p.bn; out[2] = p.tiles; out[3] = p.splits;
 }
 
-size_t conv_wgrad_ws_floats_v2(const ConvShape& s, bool deterministic) {
+size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
   if (!deterministic) return 0;
   const WgPlan p = plan_wg(s, true);
   if (p.splits <= 1) return 0;
@@ -739,7 +739,7 @@ static void run_wh(const WhArgs& a, int nb, hipStream_t st) {
   wg_check("wgrad_halo3_kernel");
 }
 
-void launch_conv_wgrad_v2(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
+void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
                           const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
                           float* zero, int zero_n) {
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");

@@ -28,27 +28,27 @@ from ..utils.seed import deterministic
 from ._ext import native
 
 _CPU_DTYPE = torch.float32  # activation dtype of the CPU reference path
-# debugging switches for the fused backward (default on): BN backward inside the dgrad epilogue,
-# and its cross-block handoff
-_FUSE_DGRAD_BN = os.environ.get("PDT_DGRAD_BN", "1") != "0"
-_BN_HANDOFF = os.environ.get("PDT_BN_HANDOFF", "1") != "0"
-_ZMASK = os.environ.get("PDT_ZMASK", "1") != "0"  # 1-bit ReLU masks for the handoff (else read z)
+# fused-backward switches (module constants; the unfused paths stay for the CPU reference and
+# the fallbacks): BN backward inside the dgrad epilogue, and its cross-block handoff
+_FUSE_DGRAD_BN = True
+_BN_HANDOFF = True
+_ZMASK = True  # 1-bit ReLU masks for the handoff (else read z)
 _NAN_TRACE = os.environ.get("PDT_NAN_TRACE", "0") == "1"  # debug: report NaN in saved tensors
 _FP8 = False  # forward convolutions on the MX-rate fp8 MFMA (set_fp8)
-_FP8_BWD = os.environ.get("PDT_FP8_BWD", "1") != "0"  # with fp8: also the input-gradient GEMMs
+_FP8_BWD = True  # with fp8: also the input-gradient GEMMs
 # with fp8 backward: weight gradients on the MX-rate MFMA from the e5m2 dy and the e4m3 conv input
 # the forward already produced (igemm_tn_f8_kernel); deterministic runs keep the bf16 slab path
-_FP8_WGRAD = os.environ.get("PDT_FP8_WGRAD", "1") != "0"
+_FP8_WGRAD = True
 # fp8-only storage: activations / input gradients whose every consumer reads the fp8 copy are not
 # written in bf16 at all (interior bottleneck outputs, and dy of convs with fp8 dgrad + fp8 wgrad)
-_FP8_ONLY = os.environ.get("PDT_FP8_ONLY", "1") != "0"
-# PDT_BN_ACC (non-deterministic runs only; deterministic runs always take the partial buffers):
+_FP8_ONLY = True
+# _BN_ACC (non-deterministic runs only; deterministic runs always take the partial buffers):
 # BN-backward sums of a BN-fused dgrad accumulated by its epilogue's fp32 atomics into a per-BN
 # [2, C] buffer -- no partial buffer and no reduce launch on the main stream; the consuming apply
 # adds the BN parameter gradients, and the buffer is re-zeroed on the weight-gradient side stream
 # once the apply is done.  Round 3 measured it neutral (r3t); with round 4's kernels it pays
-# (r4ab, interleaved, with PDT_NTQ=3: 18.78 / 18.72 ms on vs 18.86 / 18.85 off), so on by default.
-_BN_ACC = os.environ.get("PDT_BN_ACC", "1") == "1"
+# (r4ab, interleaved: 18.78 / 18.72 ms on vs 18.86 / 18.85 off), so on.
+_BN_ACC = True
 
 
 def _bacc(p, c):
@@ -58,12 +58,12 @@ def _bacc(p, c):
         a = torch.zeros(2, c, dtype=torch.float32, device=p.device)
         p._pdt_bacc = a
     return a
-_FUSE_RES_BN = os.environ.get("PDT_RES_BN", "1") != "0"  # shortcut BN applied in the block tail
+_FUSE_RES_BN = True  # shortcut BN applied in the block tail
 # test hook (tests/test_blocks_gpu.py, mask-matched reference): when a list, every fused block
 # forward appends its units' stored post-activation outputs (z, NHWC bf16), so an fp32 reference
 # can take the native path's ReLU decisions and compare gradients without ReLU-flip noise
 _CAPTURE = None
-_COMPACT_ADDEND = os.environ.get("PDT_COMPACT_ADDEND", "1") != "0"  # stride-2 shortcut dgrad compact
+_COMPACT_ADDEND = True  # stride-2 shortcut dgrad compact
 
 
 def set_fp8(on: bool) -> None:
@@ -420,9 +420,9 @@ class _StemConvBNPool(torch.autograd.Function):
         return (None, dw, dgamma, dbeta, None, None, None, None, None, None, None)
 
 
-_STEM_POOL = os.environ.get("PDT_STEM_POOL", "1") != "0"  # debugging switch (default on)
-_STEM_BWD_FUSED = os.environ.get("PDT_STEM_BWD_FUSED", "1") != "0"  # A/B switch (default on)
-_STEM_ARGMAX_Y = os.environ.get("PDT_STEM_ARGMAX_Y", "1") != "0"  # A/B switch (default on)
+_STEM_POOL = True  # debugging switch (default on)
+_STEM_BWD_FUSED = True  # A/B switch (default on)
+_STEM_ARGMAX_Y = True  # A/B switch (default on)
 
 
 def _stem_fast(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -745,11 +745,11 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     return z, y, stats, None, None
 
 
-_FP8_KMIN = int(os.environ.get("PDT_FP8_KMIN", "128"))
+_FP8_KMIN = 128
 
 
 def _fp8_conv_ok(r, s, cx):
-    """fp8 forward conv for a GEMM K of r*s*cx >= PDT_FP8_KMIN (K = 64 half-fills the 128-wide fp8
+    """fp8 forward conv for a GEMM K of r*s*cx >= _FP8_KMIN (K = 64 half-fills the 128-wide fp8
     K-step).  128 (layer2's 1x1 over 128 channels on fp8, so its input needs no bf16 copy) vs 256:
     fp8 b512 31.23 vs 31.39 ms, b256 17.04 vs 17.01 ms (r3p, one box).  64 (every layer-1 1x1 on
     fp8 too, after the narrow fp8 dgrad) vs 128: b256 16.88 vs 16.77 ms, b512 31.09 vs 30.83 ms
@@ -757,12 +757,12 @@ def _fp8_conv_ok(r, s, cx):
     return r * s * cx >= _FP8_KMIN
 
 
-_FP8_DGRAD_NARROW = os.environ.get("PDT_FP8_DGRAD_NARROW", "1") != "0"
+_FP8_DGRAD_NARROW = True
 
 
 def _fp8_dgrad_ok(k, stride):
     """fp8 input gradient for a dy of k channels: whole 128-byte K-steps per tap (k % 128), or
-    (PDT_FP8_DGRAD_NARROW, default on) any k % 16 at stride 1 -- the 64-channel layer-1 convs, whose
+    (_FP8_DGRAD_NARROW) any k % 16 at stride 1 -- the 64-channel layer-1 convs, whose
     dy then needs no bf16 copy at all when the weight gradient is fp8 too."""
     return k % 128 == 0 or (_FP8_DGRAD_NARROW and stride == 1 and k % 16 == 0)
 

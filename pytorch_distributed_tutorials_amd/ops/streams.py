@@ -12,7 +12,7 @@ does not hand their memory out while the side stream still reads them -- all thr
 in one native call, ``C.conv_wgrad_side`` (csrc/bindings.cpp); gradient
 all-reduces wait for the side stream (``Reducer.set_aux_stream``); and a callback
 at the end of backward joins it into the caller's stream, so the optimizer step
-sees every gradient.  ``PDT_WGRAD_STREAM=0`` turns it off.
+sees every gradient.
 
 One join per backward pass suffices: ``begin`` queues it for the first block of a
 graph task only.  (Handing a block's wgrads over in one batch instead of one per
@@ -26,8 +26,8 @@ from typing import Dict, Optional
 
 import torch
 
-_enabled = os.environ.get("PDT_WGRAD_STREAM", "1") != "0"
-_branch_enabled = os.environ.get("PDT_BRANCH_STREAM", "1") != "0"
+_enabled = True
+_branch_enabled = True
 _streams: Dict[int, torch.cuda.Stream] = {}
 _branch_streams: Dict[int, torch.cuda.Stream] = {}
 _joined_task = [None]  # graph task whose end-of-backward join is already queued
@@ -105,7 +105,7 @@ def set_branch_enabled(on: bool) -> None:
 
 
 def branch_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
-    """Stream for the projection-shortcut branch of a downsampling block (``PDT_BRANCH_STREAM``):
+    """Stream for the projection-shortcut branch of a downsampling block :
     the shortcut conv + BN statistics in forward, and its BN backward + input gradient in
     backward, run concurrently with the main chain's first units and join before the unit that
     consumes them.  They fill the CUs the main chain's GEMMs leave idle (grids of 49 x 2^k

@@ -245,8 +245,7 @@ class DistributedDataParallel(nn.Module):
                 warnings.warn(f"{e}; gradients are reduced through torch.distributed collectives")
         # the buffer-broadcast wait can move to the first BatchNorm only where every buffer
         # reader is one of our BN kernels (ops.buffers_ready): the native device model
-        self._defer_buffer_wait = (self.comm is not None and getattr(module, "impl", None) == "native"
-                                   and os.environ.get("PDT_DEFER_BUFFER_WAIT", "1") != "0")
+        self._defer_buffer_wait = self.comm is not None and getattr(module, "impl", None) == "native"
 
         if self._collective and (self.world_size > 1 or self.comm is not None):
             self._sync_module_states()

@@ -13,7 +13,6 @@ bucket order.  Consequences:
 from __future__ import annotations
 
 import operator
-import os
 import weakref
 from typing import Dict, List, Optional, Sequence
 
@@ -126,8 +125,7 @@ class FlatParamSpace:
 
     def mirror(self) -> "Optional[WeightMirror]":
         """bf16 conv-weight mirror (GPU spaces only), created on first use."""
-        if self._mirror is None and self.param_flat.is_cuda \
-                and os.environ.get("PDT_WEIGHT_MIRROR", "1") != "0":
+        if self._mirror is None and self.param_flat.is_cuda:
             self._mirror = WeightMirror(self)
         return self._mirror
 
