@@ -1403,6 +1403,7 @@ PYBIND11_MODULE(_C, m) {
     const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
     return out.narrow(0, 0, got);
   }, py::arg("n"));
+  m.def("conv_nt_force", &pdt::conv_nt_force, py::arg("k32") = -1, py::arg("mid") = -1);
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);

@@ -68,6 +68,9 @@ class AbortGate {
     }
   }
 
+  // false once the communicator has been aborted (or finalized)
+  bool usable() const { return !aborted_.load(); }
+
   // Blocking form for teardown: waits for an in-flight call, then runs f (destroy/abort) once
   // unless the communicator was already aborted.
   template <class F>

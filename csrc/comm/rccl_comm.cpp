@@ -284,13 +284,20 @@ void RcclComm::track(const char* what) {
   pending_.push_back({ev, std::chrono::steady_clock::now(), what});
 }
 
+// Non-blocking communicator: the enqueue returned ncclInProgress.  Poll its completion with ONE
+// ncclCommGetAsyncError per gate call, so the gate is free between polls: an abort requested by
+// the monitor, the watchdog or the user runs between two polls (RCCL allows ncclCommAbort to
+// cancel an in-progress non-blocking operation) instead of waiting out the whole poll.
+// Returns ncclInProgress on timeout and ncclInvalidUsage when the communicator was aborted.
 ncclResult_t RcclComm::wait_async(const char* what) {
-  // non-blocking communicator: the call completes asynchronously (runs inside the gate)
   (void)what;
   const auto t0 = std::chrono::steady_clock::now();
   ncclResult_t st = ncclInProgress;
   while (st == ncclInProgress) {
-    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+    const bool ran = gate_->call([&]() {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+    });
+    if (!ran) return ncclInvalidUsage;  // aborted between polls
     if (st == ncclInProgress && since(t0) > opt_.init_timeout_s) break;
     if (st == ncclInProgress) std::this_thread::yield();
   }
@@ -301,14 +308,13 @@ template <class F>
 void RcclComm::issue(const char* what, F&& enqueue) {
   check();
   ncclResult_t r = ncclSuccess;
-  const bool ran = gate_->call([&]() {
-    r = enqueue();
-    if (r == ncclInProgress) r = wait_async(what);
-  });
-  if (!ran) {  // aborted between check() and the gate: refuse with the recorded error
+  const bool ran = gate_->call([&]() { r = enqueue(); });
+  const bool aborted_in_poll = ran && r == ncclInProgress && (r = wait_async(what)) == ncclInvalidUsage &&
+                               !gate_->usable();
+  if (!ran || aborted_in_poll) {  // aborted before or while the call completed: the recorded error
     check();
     throw std::runtime_error(std::string("RCCL communicator (rank ") + std::to_string(rank_) +
-                             ") was aborted before " + what);
+                             ") was aborted " + (ran ? "while completing " : "before ") + what);
   }
   if (r == ncclInProgress) {
     fail(std::string(what) + " still in progress after the init timeout");

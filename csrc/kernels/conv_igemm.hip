@@ -1576,7 +1576,13 @@ static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
 // 256->64 117 -> 103, and the 64-channel dgrads -- while every long-K conv loses 5-20% to the
 // doubled barriers and fragment-read restarts (256x14x14 3x3 68 -> 79 us).  Policy: K32 for
 // M >= 786432 on forward (stats epilogue) GEMMs and 64-column dgrads.
+// Test hook (conv_nt_force): pin the K32 / K64 main loop of every NT launch, or disable the
+// 128x256 short-K tile, so tests can compare the policy's alternatives bit for bit.  -1: policy.
+static int g_force_k32 = -1, g_force_mid = -1;
+void conv_nt_force(int k32, int mid) { g_force_k32 = k32; g_force_mid = mid; }
+
 static bool nt_k32(const NtArgs& a, int epi) {
+  if (g_force_k32 >= 0) return g_force_k32 == 1;
   return a.M >= 786432 && (epi == EPI_STATS || a.Nout <= 64);
 }
 
@@ -1600,6 +1606,7 @@ static bool use_wide_tile(int M, int Nout, int kg_bytes) {
 // (off) -> 18.94 (K <= 512) / 18.95 (K <= 256) / 19.06 (K <= 1024); isolated fwd 4.22 -> 4.16 ms,
 // BN-fused dgrad 5.65 -> 5.52 ms.
 static bool use_mid_tile(int M, int Nout, int kg_bytes) {
+  if (g_force_mid == 0) return false;
   constexpr int kmax = 512;
   return M > 8192 && Nout % 256 == 0 && kg_bytes <= 2 * kmax;
 }

@@ -51,6 +51,25 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint
       r, (__attribute__((address_space(3))) void*)(reinterpret_cast<uintptr_t>(lds)), 16, voff, 0, 0, 0);
 }
 
+// The LDS-DMA as inline asm, for kernels that read their tiles with ds_read_b64_tr_b16: hipcc
+// puts an `s_waitcnt vmcnt(0)` in front of every LDS read it cannot prove disjoint from a pending
+// LDS-DMA it knows about, which drains a multi-stage ring at every fragment read.  Issued through
+// asm, the DMA is invisible to that analysis; the kernel orders it with its own counted vmcnt +
+// barrier (a compiler-placed vmcnt for its own loads only ever waits for more, never less).  `r`
+// is the buffer descriptor (rsrc_words), `lds` the wave-uniform LDS byte address of the 1-KiB
+// destination.
+__device__ __forceinline__ v4i rsrc_words(const void* p, uint32_t num_bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return v4i{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xffffu), (int)num_bytes, 0x00020000};
+}
+__device__ __forceinline__ void glds16_asm(const v4i& r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds"
+               :: "v"(voff), "s"(__builtin_amdgcn_readfirstlane(lds)), "s"(r) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+
 // Wait until at most N of this wave's vector-memory ops (LDS-DMA included) are outstanding.
 template <int N>
 __device__ __forceinline__ void wait_vm() {

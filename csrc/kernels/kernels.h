@@ -67,6 +67,8 @@ struct ConvShape {
 int conv_nt_group_rows(int M, int Nout, int kg_bytes);
 // (BM, BN) of the NT workgroup tile the fwd / dgrad launch of such a GEMM runs (test introspection)
 void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn);
+// tests: force the NT main loop (k32 1 / 0) and disable the 128x256 tile (mid 0); -1 = policy
+void conv_nt_force(int k32, int mid);
 // number of stream-K NT launches so far in this process (tests: which path ran)
 // PDT_NT_TIMING builds (scripts/build_variant.sh): per-workgroup phase timestamps of NT launches
 // (s_memtime at start / first operands in LDS / main loop done / epilogue stats done / end, plus

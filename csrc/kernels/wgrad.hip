@@ -103,8 +103,9 @@ __global__ void __launch_bounds__(512, 2) wgrad_kernel(const WgArgs P) {
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
+  const v4i rdy = rsrc_words(P.dy, P.dy_bytes);
+  const v4i rx = rsrc_words(P.x, P.x_bytes);
+  const uint32_t sbase = lds_addr(smem);
 
   // A (dy): piece p of wave w covers rows (w*A_PW + p)*A_RPI + lane/A_LPR; LDS slot lane%A_LPR of a
   // row holds source chunk swz(slot) (the XOR is an involution), so the lane-linear DMA image IS
@@ -149,13 +150,13 @@ __global__ void __launch_bounds__(512, 2) wgrad_kernel(const WgArgs P) {
   }
 
   auto issue = [&](int step, int buf) {
-    char* As = smem + buf * CFG::STAGE;
-    char* Bs = As + CFG::A_BYTES;
+    const uint32_t As = sbase + buf * CFG::STAGE;
+    const uint32_t Bs = As + CFG::A_BYTES;
     const int mb = step * 64;
     const int abase = mb * P.Kout * 2;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i)
-      glds16(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
+      glds16_asm(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
       uint32_t off;
@@ -177,7 +178,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_kernel(const WgArgs P) {
         b_ho[i] = c2 ? ho - (uint32_t)P.Ho : ho;
         b_n[i] += (uint32_t)P.adv_qn + c2;
       }
-      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
+      glds16_asm(rx, Bs + (wid * B_PW + i) * 1024, off);
     }
   };
 
@@ -199,43 +200,60 @@ __global__ void __launch_bounds__(512, 2) wgrad_kernel(const WgArgs P) {
     return base + swz_img<CFG::B_ROWB>(row, col >> 3) + ((col & 7) << 1);
   };
 
-  // ring of ST K64 slots: slot j lives in buffer j % ST.  Iteration j: wait until step j landed
-  // (the ST-2 younger steps may stay in flight), barrier (RAW for slot j; WAR for buffer
-  // (j+ST-1) % ST = (j-1) % ST, whose fragment reads every wave retired before the barrier:
-  // lds_barrier_rd), refill that buffer with step j+ST-1, compute step j.
+  // Ring of ST K64 slots, slot j in buffer j % ST, fragments read ONE step ahead: iteration j waits
+  // until step j+1 landed, passes the barrier (RAW for slot j+1; WAR for buffer (j+ST-1) % ST =
+  // (j-1) % ST, whose fragments were read in iteration j-2 and consumed by the MFMAs of iteration
+  // j-1), refills that buffer with step j+ST-1, issues the reads of slot j+1 and runs the MFMAs of
+  // step j on the fragments read one iteration earlier -- the LDS reads of the next step overlap
+  // the MFMAs of this one (the compiler places the lgkmcnt waits: the reads are builtins, only the
+  // DMA is asm).  Two fragment sets, the loop unrolled by two, so no register copies.
   const int nst = s_end - s_begin;
 #pragma unroll
   for (int p = 0; p < ST - 1; ++p)
     if (p < nst) issue(s_begin + p, p);
   const int rowA = half * 32 + 8 * g + tq;  // m row of this wave's first tr block
-  for (int j = 0; j < nst; ++j) {
-    wait_steps<LPS>(min(nst - 1, j + ST - 2) - j);
-    lds_barrier_rd();
-    if (j + ST - 1 < nst) issue(s_begin + j + ST - 1, (j + ST - 1) % ST);
+  auto read = [&](int j, v4i (&af)[4], v4i (&bfr)[4]) {
     const char* As = smem + (j % ST) * CFG::STAGE;
     const char* Bs = As + CFG::A_BYTES;
-    v4i af[4], bfr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = wm * 64 + i * 16 + 4 * tp;
       const char* pa = frag_a(As, rowA, col);  // row + 4: same swizzle class, +4 rows of bytes
-      af[i] = cat_frag(ds_read_tr_asm(pa), ds_read_tr_asm<4 * CFG::A_ROWB>(pa));
+      af[i] = cat_frag(ds_read_tr(pa), ds_read_tr(pa + 4 * CFG::A_ROWB));
     }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int col = wn * 64 + jj * 16 + 4 * tp;
       const char* pb = frag_b(Bs, rowA, col);
-      bfr[jj] = cat_frag(ds_read_tr_asm(pb), ds_read_tr_asm<4 * CFG::B_ROWB>(pb));
+      bfr[jj] = cat_frag(ds_read_tr(pb), ds_read_tr(pb + 4 * CFG::B_ROWB));
     }
-    // the asm reads are asynchronous: retire them before the MFMAs consume the fragments (tying
-    // the fragments to the wait keeps the compiler from hoisting an MFMA above it)
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]),
-                   "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]), "+v"(bfr[3]));
+  };
+  auto body = [&](int j, v4i (&af)[4], v4i (&bfr)[4], v4i (&an)[4], v4i (&bn)[4]) {
+    // this body's fragments (read by the previous body) have landed: a compiler-visible
+    // lgkmcnt(0), so the waitcnt pass knows it and places no wait on the newer reads in front of
+    // the MFMAs below (it cannot count 32 reads in flight -- lgkmcnt holds 15 -- and would stall
+    // them behind the next step's reads)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (j + 1 < nst) {
+      wait_steps<LPS>(min(nst - 1, j + ST - 2) - (j + 1));
+      lds_barrier_rd();
+      if (j + ST - 1 < nst) issue(s_begin + j + ST - 1, (j + ST - 1) % ST);
+      read(j + 1, an, bn);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mfma16(af[i], bfr[jj], acc[i][jj]);
+  };
+  v4i fa0[4], fb0[4], fa1[4], fb1[4];
+  if (nst > 0) {
+    wait_steps<LPS>(min(nst - 1, ST - 2));
+    lds_barrier_rd();
+    read(0, fa0, fb0);
+  }
+  for (int j = 0; j < nst; j += 2) {
+    body(j, fa0, fb0, fa1, fb1);
+    if (j + 1 < nst) body(j + 1, fa1, fb1, fa0, fb0);
   }
   __syncthreads();  // every DMA landed (last wait was vmcnt(0)) and every fragment read retired
 
@@ -387,8 +405,9 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
+  const v4i rdy = rsrc_words(P.dy, P.dy_bytes);
+  const v4i rx = rsrc_words(P.x, P.x_bytes);
+  const uint32_t sbase = lds_addr(smem);
 
   // the two zero rows after every B slot (never DMA targets); the first loop barrier publishes them
   for (int i = t; i < ST * (2 * CFG::B_ROWB / 16); i += 512) {
@@ -439,15 +458,15 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
   };
 
   auto issue = [&](int buf) {
-    char* As = smem + buf * CFG::STAGE;
-    char* Bs = As + CFG::A_BYTES;
+    const uint32_t As = sbase + buf * CFG::STAGE;
+    const uint32_t Bs = As + CFG::A_BYTES;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) {
       // output pixel (n, h, w) exists for h < H, w < W; the padded ones carry dy = 0
       const bool ok = a_h[i] < (uint32_t)P.H && a_w[i] < (uint32_t)P.W;
       const uint32_t pix = __umul24(a_n[i], (uint32_t)HW) + __umul24(a_h[i], (uint32_t)P.W) + a_w[i];
       const uint32_t off = ok ? __umul24(pix, (uint32_t)K2) + (uint32_t)a_kb[i] : OOB;
-      glds16(rdy, As + (wid * A_PW + i) * 1024, off);
+      glds16_asm(rdy, As + (wid * A_PW + i) * 1024, off);
       advance(a_n[i], a_h[i], a_w[i]);
     }
 #pragma unroll
@@ -456,7 +475,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
       const bool ok = b_g[i] >= 1u && b_w[i] >= 1u && b_w[i] <= (uint32_t)P.W;
       const uint32_t pix = __umul24(b_n[i], (uint32_t)HW) + __umul24(b_g[i] - 1u, (uint32_t)P.W) + (b_w[i] - 1u);
       const uint32_t off = ok ? __umul24(pix, (uint32_t)C2) + (uint32_t)b_cb[i] : OOB;
-      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
+      glds16_asm(rx, Bs + (wid * B_PW + i) * 1024, off);
       advance(b_n[i], b_g[i], b_w[i]);
     }
   };
@@ -472,23 +491,20 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
+  // the ring as in wgrad_kernel: fragments read one step ahead, two fragment sets, unrolled by two
   const int nst = s_end - s_begin;
 #pragma unroll
   for (int p = 0; p < ST - 1; ++p)
     if (p < nst) issue(p);
   const int rowA = half * 32 + 8 * g + tq;
-  for (int j = 0; j < nst; ++j) {
-    wait_younger<LPS, ST - 2>(min(nst - 1, j + ST - 2) - j);
-    lds_barrier_rd();
-    if (j + ST - 1 < nst) issue((j + ST - 1) % ST);
+  auto read = [&](int j, v4i (&af)[4], v4i (&bfr)[NB]) {
     const char* As = smem + (j % ST) * CFG::STAGE;
     const char* Bs = As + CFG::A_BYTES;
-    v4i af[4], bfr[NB];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = wm * 64 + i * 16 + 4 * tp;
       const char* pa = As + swz_img<CFG::A_ROWB>(rowA, col >> 3) + ((col & 7) << 1);
-      af[i] = cat_frag(ds_read_tr_asm(pa), ds_read_tr_asm<4 * CFG::A_ROWB>(pa));
+      af[i] = cat_frag(ds_read_tr(pa), ds_read_tr(pa + 4 * CFG::A_ROWB));
     }
 #pragma unroll
     for (int s = 0; s < 3; ++s)
@@ -496,22 +512,32 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
       for (int c = 0; c < TC; ++c) {
         const int col = wc * 16 * TC + c * 16 + 4 * tp;
         const int rb = rowA + s;  // tap s: the image shifted by s rows (swizzle differs at rb + 4)
-        bfr[s * TC + c] = cat_frag(ds_read_tr_asm(Bs + swz_img<CFG::B_ROWB>(rb, col >> 3) + ((col & 7) << 1)),
-                                   ds_read_tr_asm(Bs + swz_img<CFG::B_ROWB>(rb + 4, col >> 3) + ((col & 7) << 1)));
+        bfr[s * TC + c] = cat_frag(ds_read_tr(Bs + swz_img<CFG::B_ROWB>(rb, col >> 3) + ((col & 7) << 1)),
+                                   ds_read_tr(Bs + swz_img<CFG::B_ROWB>(rb + 4, col >> 3) + ((col & 7) << 1)));
       }
-    if constexpr (TC == 1) {
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]));
-    } else {
-      static_assert(TC == 2, "TC");
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bfr[0]), "+v"(bfr[1]),
-                     "+v"(bfr[2]), "+v"(bfr[3]), "+v"(bfr[4]), "+v"(bfr[5]));
+  };
+  auto body = [&](int j, v4i (&af)[4], v4i (&bfr)[NB], v4i (&an)[4], v4i (&bn)[NB]) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this body's fragments landed (see wgrad_kernel)
+    if (j + 1 < nst) {
+      wait_younger<LPS, ST - 2>(min(nst - 1, j + ST - 2) - (j + 1));
+      lds_barrier_rd();
+      if (j + ST - 1 < nst) issue((j + ST - 1) % ST);
+      read(j + 1, an, bn);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int n = 0; n < NB; ++n) acc[i][n] = mfma16(af[i], bfr[n], acc[i][n]);
+  };
+  v4i fa0[4], fb0[NB], fa1[4], fb1[NB];
+  if (nst > 0) {
+    wait_younger<LPS, ST - 2>(min(nst - 1, ST - 2));
+    lds_barrier_rd();
+    read(0, fa0, fb0);
+  }
+  for (int j = 0; j < nst; j += 2) {
+    body(j, fa0, fb0, fa1, fb1);
+    if (j + 1 < nst) body(j + 1, fa1, fb1, fa0, fb0);
   }
   __syncthreads();
 
@@ -571,27 +597,48 @@ __global__ void __launch_bounds__(512, 2) wgrad_halo3_kernel(const WhArgs P) {
   }
 }
 
-__global__ void __launch_bounds__(256) wg_splitk_reduce_kernel(const float* __restrict__ ws, int splits,
-                                                            int64_t n, float* __restrict__ out,
-                                                            int accumulate) {
-  int64_t n4 = n / 4;
-  int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 s = reinterpret_cast<const float4*>(ws)[i];
-    for (int k = 1; k < splits; ++k) {
-      float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n)[i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+// Fixed-order sum of the split-K slabs: ws[splits][n4] float4 -> out[n4].  A 256-thread block
+// owns 16 float4 columns; thread (column c, lane k) sums slabs k, k+16, k+32, ... in order, and the
+// 16 partials of a column are added in k order through LDS -- the same summation tree on every
+// run (bitwise deterministic), with 16x more loads in flight than one thread per column (the
+// layer-1 weight gradients have ~256 slabs of only 16K floats).
+__global__ void __launch_bounds__(256) wg_splitk_reduce_kernel(const float4* __restrict__ ws, int splits,
+                                                               int64_t n4, float4* __restrict__ out,
+                                                               int accumulate) {
+  __shared__ float4 part[16][17];
+  const int c = threadIdx.x & 15, k = threadIdx.x >> 4;
+  const int64_t col = (int64_t)blockIdx.x * 16 + c;
+  float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+    int i = k;
+#pragma unroll 1
+    for (; i + 48 < splits; i += 64) {  // four slabs in flight per thread, added in slab order
+      const float4 v0 = ws[(int64_t)i * n4 + col], v1 = ws[(int64_t)(i + 16) * n4 + col];
+      const float4 v2 = ws[(int64_t)(i + 32) * n4 + col], v3 = ws[(int64_t)(i + 48) * n4 + col];
+      sm.x += v0.x; sm.y += v0.y; sm.z += v0.z; sm.w += v0.w;
+      sm.x += v1.x; sm.y += v1.y; sm.z += v1.z; sm.w += v1.w;
+      sm.x += v2.x; sm.y += v2.y; sm.z += v2.z; sm.w += v2.w;
+      sm.x += v3.x; sm.y += v3.y; sm.z += v3.z; sm.w += v3.w;
+    }
+    for (; i < splits; i += 16) {
+      const float4 v = ws[(int64_t)i * n4 + col];
+      sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+    }
+  }
+  part[k][c] = sm;
+  __syncthreads();
+  if (k == 0 && col < n4) {
+    float4 t = part[0][c];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      const float4 v = part[q][c];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
     if (accumulate) {
-      float4 o = reinterpret_cast<float4*>(out)[i];
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+      const float4 o = out[col];
+      t.x += o.x; t.y += o.y; t.z += o.z; t.w += o.w;
     }
-    reinterpret_cast<float4*>(out)[i] = s;
-  }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(int64_t)k * n + i];
-    out[i] = accumulate ? out[i] + s : s;
+    out[col] = t;
   }
 }
 
@@ -608,6 +655,7 @@ struct WgPlan {
   int kind, wm, wn, tc;         // tile layout: 4 wave pairs as wm x wn (x tc channel blocks: HALO3)
   int bm, bn;                   // tile rows (output channels) x columns (dW columns)
   int tiles, splits, steps_per_split, nsteps;
+  bool slab;                    // split-K partials in private slabs + fixed-order reduce (else atomics)
 };
 
 // Tuning knobs: PDT_WG_CUS (CUs the split-K plan fills, default: the device's), PDT_WG_HALO=0
@@ -640,7 +688,7 @@ static bool wg_halo_on() {
 // in ceil(tiles * splits / CUs) rounds of ceil(nsteps / splits) K-steps, and every block flushes
 // its fp32 tile (atomics at ~1.3 TB/s chip-wide, MI355X_MICROARCH; slabs at the store rate).
 // Minimise rounds * steps * t_step + flush + a per-round ramp.
-static int choose_splits(int tiles, int nsteps, double t_step_us, double tile_bytes, bool slab) {
+static int choose_splits(int tiles, int nsteps, double t_step_us, double tile_bytes, bool slab, double* est_us) {
   const int cus = wg_cus();
   const double flush_bw = slab ? 5.0e6 : 1.3e6;  // bytes per us
   int best = 1;
@@ -651,9 +699,12 @@ static int choose_splits(int tiles, int nsteps, double t_step_us, double tile_by
     const int eff = (nsteps + sps - 1) / sps;  // splits actually launched
     if (eff != sp) continue;
     const int rounds = (tiles * sp + cus - 1) / cus;
-    const double t = rounds * (sps * t_step_us + 2.0) + tiles * (double)sp * tile_bytes / flush_bw;
+    double t = rounds * (sps * t_step_us + 2.0) + tiles * (double)sp * tile_bytes / flush_bw;
+    // slabs: the fixed-order reduce pass reads every slab and read-modify-writes dW (+ a launch)
+    if (slab && sp > 1) t += (sp + 2) * (tiles * tile_bytes) / 5.0e6 + 3.0;
     if (t < best_t - 1e-9) { best_t = t; best = sp; }
   }
+  *est_us = best_t;
   return best;
 }
 
@@ -691,13 +742,26 @@ static WgPlan plan_wg(const ConvShape& s, bool deterministic) {
   mfma_cyc = (double)p.bm * p.bn * 64 * 2 / 4096.0;  // per K-step per CU at the MFMA peak
   // a K-step's cost: its MFMAs at ~50 % of peak, or its LDS-DMA bytes at ~50 GB/s per CU
   const double t_step = std::max(mfma_cyc * 2.0 / 2400.0, stage_bytes / 50.0e3);
-  int splits = choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, deterministic);
-  if (deterministic) {  // slab workspace: splits * |dW| * 4 bytes, capped at 64 MB
+  // split-K reduction: fp32 atomics (~1.3 TB/s, memory side) or private slabs written at the store
+  // rate plus a fixed-order reduce launch, whichever the model prices lower; deterministic runs
+  // always take the slabs (bitwise run to run)
+  double t_atomic = 1e30, t_slab = 1e30;
+  const int s_slab = choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, true, &t_slab);
+  const int s_atomic = deterministic ? 1 : choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, false, &t_atomic);
+  static int force_slab = -2;
+  if (force_slab == -2) {
+    const char* e = getenv("PDT_WG_SLAB");  // A/B: 0 atomics, 1 slabs (non-deterministic runs)
+    force_slab = e ? atoi(e) : -1;
+  }
+  p.slab = deterministic || (force_slab >= 0 ? force_slab == 1 : t_slab < t_atomic);
+  int splits = p.slab ? s_slab : s_atomic;
+  if (p.slab) {  // slab workspace: splits * |dW| * 4 bytes, capped at 64 MB
     const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
     splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, ((int64_t)64 << 20) / dw_bytes));
   }
   p.steps_per_split = (p.nsteps + splits - 1) / splits;
   p.splits = (p.nsteps + p.steps_per_split - 1) / p.steps_per_split;
+  if (p.splits <= 1) p.slab = false;
   return p;
 }
 
@@ -707,9 +771,8 @@ void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]) {
 }
 
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic) {
-  if (!deterministic) return 0;
-  const WgPlan p = plan_wg(s, true);
-  if (p.splits <= 1) return 0;
+  const WgPlan p = plan_wg(s, deterministic);
+  if (!p.slab) return 0;
   return (size_t)p.splits * s.K * s.R * s.S * s.C;
 }
 
@@ -744,8 +807,9 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
                           float* zero, int zero_n) {
   if (s.C % 8 != 0 || s.K % 8 != 0) throw std::runtime_error("conv_wgrad: channels must be multiples of 8");
   const WgPlan p = plan_wg(s, deterministic);
-  const bool slab = deterministic && p.splits > 1;
-  const bool atomic = !deterministic && p.splits > 1;
+  const bool slab = p.slab;
+  const bool atomic = !p.slab && p.splits > 1;
+  if (slab && ws == nullptr) throw std::runtime_error("conv_wgrad: the slab plan needs its workspace");
   const int mode = atomic ? WG_ATOMIC : (slab ? WG_STORE : (accumulate ? WG_ACCUM : WG_STORE));
   const int64_t n = (int64_t)s.K * s.R * s.S * s.C;
   if (atomic && !accumulate) hipMemsetAsync(dw, 0, n * sizeof(float), st);
@@ -797,9 +861,11 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
     else { if (pw) run_wg<4, 1, true>(a, nb, st); else run_wg<4, 1, false>(a, nb, st); }
   }
   if (slab) {
-    int64_t b = (n / 4 + 255) / 256;
-    hipLaunchKernelGGL(wg_splitk_reduce_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(b, 4096))),
-                       dim3(256), 0, st, ws, p.splits, n, dw, accumulate ? 1 : 0);
+    if (n % 4 != 0) throw std::runtime_error("conv_wgrad: dW size must be a multiple of 4 floats");
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(wg_splitk_reduce_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(ws), p.splits, n4, reinterpret_cast<float4*>(dw),
+                       accumulate ? 1 : 0);
     wg_check("splitk_reduce");
   }
 }

@@ -328,6 +328,15 @@ class _StemConvBN(torch.autograd.Function):
                 None, None, None)
 
 
+def _end_mirror_trust(weight) -> None:
+    """The stem's backward is the native model's last backward node: end the bf16 weight mirror's
+    per-step trust (parallel/flat.py WeightMirror.end_trust)."""
+    sp = getattr(weight, "_pdt_flat", None)
+    m = getattr(sp, "_mirror", None) if sp is not None else None
+    if m is not None:
+        m.end_trust()
+
+
 class _StemConvBNPool(torch.autograd.Function):
     """_StemConvBN followed by the 3x3/s2/p1 max pool in ONE fused BN-apply/ReLU/pool pass.
 
@@ -404,6 +413,7 @@ class _StemConvBNPool(torch.autograd.Function):
                                       deterministic()).to(weight.dtype)
             if sunk:
                 sunk[0]._pdt_flat.mark_ready(sunk)
+            _end_mirror_trust(weight)
             ctx.weight = None
             return (None, dw, dgamma, dbeta, None, None, None, None, None, None, None)
         dy = C.pool_bn_bwd_apply(dout, idx, y, stats, gamma, sums, ctx.training)
@@ -416,6 +426,7 @@ class _StemConvBNPool(torch.autograd.Function):
                 dw = C.stem_wgrad(dy, xsp, list(weight.shape), deterministic()).to(weight.dtype)
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
+        _end_mirror_trust(weight)
         ctx.weight = None
         return (None, dw, dgamma, dbeta, None, None, None, None, None, None, None)
 

@@ -309,6 +309,13 @@ class WeightMirror:
             self.refresh()
         self._trusted = self.key
 
+    def end_trust(self) -> None:
+        """The native backward's last node (the stem) ran: the trust ensure() granted ends here, so
+        it lasts exactly one forward/backward.  An optimizer other than the fused SGD, or an
+        in-place weight edit (load_state_dict, clipping) before the next forward, is then caught
+        by the version-counter check of the next view taken outside the model's forward."""
+        self._trusted = None
+
     def after_optimizer_step(self) -> None:
         """The fused SGD step just wrote ``krsc``; rebuild ``crsk`` and mark both current."""
         self.space.version += 1

@@ -37,3 +37,20 @@ def test_ddp_two_ranks_one_gpu(tmp_path, gpu):
         assert x["launch_order"] == list(range(x["bucket_info"]["num_buckets"]))
     cs = res[0]["checksums"]
     assert cs[0] == cs[1], cs
+
+
+def test_bench_two_ranks_share_device_ranks_identical(tmp_path, gpu):
+    """bench.py at N>1 proves its ranks ended bit-identical (all-gathered
+    parameter checksum in the JSON) -- rehearsed with 2 gloo ranks sharing cuda:0 on the native
+    kernels, the same bench path the driver's 8-GPU run takes."""
+    out = tmp_path / "b.json"
+    env = dict(os.environ, MASTER_PORT=str(free_port()), OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
+                        "--backend", "gloo", "--arch", "resnet18", "--image-size", "64", "--batch", "16",
+                        "--steps", "2", "--warmup", "1", "--json-out", str(out)],
+                       cwd=ROOT, env=env, timeout=110, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["n_gpus"] == 2 and d["config"]["shared_device"]
+    assert d["config"]["ranks_identical"] is True, d["config"]

@@ -379,6 +379,7 @@ sys.path.insert(0, sys.argv[1] + "/tests")
 from pytorch_distributed_tutorials_amd.ops import native
 from test_tiles_gpu import FWD_TILES, DGRAD_TILES, _operands
 C = native()
+C.conv_nt_force(int(sys.argv[3]), int(sys.argv[4]))
 dev = torch.device("cuda:0")
 out = {}
 for i, (shape, _) in enumerate(FWD_TILES):
@@ -407,10 +408,9 @@ def test_k32_ring_bitwise_equals_k64_double_buffer(gpu, tmp_path):
     the K64 double buffer (two K=32 MFMAs per 64-deep step), so forced-K32 and forced-K64 runs of
     every tile must agree bit for bit -- outputs, BN partials and BN-backward sums."""
     res = {}
-    for mode, env_add in (("0", {"PDT_NT_K32": "0"}), ("1", {"PDT_NT_K32": "1"}), ("mid0", {"PDT_NT_MID": "0"})):
-        env = dict(os.environ, **env_add)
+    for mode, force in (("0", ("0", "-1")), ("1", ("1", "-1")), ("mid0", ("0", "0"))):
         f = str(tmp_path / f"k32_{mode}.pt")
-        r = subprocess.run([sys.executable, "-c", _K32_SCRIPT, ROOT, f], env=env, capture_output=True,
+        r = subprocess.run([sys.executable, "-c", _K32_SCRIPT, ROOT, f, *force], capture_output=True,
                            text=True, timeout=110)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         res[mode] = torch.load(f, weights_only=True)
