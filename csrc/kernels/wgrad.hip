@@ -14,17 +14,26 @@
 //     atomics: every wgrad flushed ~32 MB of them, ~25 us of the memory-side atomic rate
 //     (MI355X_MICROARCH "Global float atomics": ~1.3 TB/s chip-wide) at the end of a 60-140 us
 //     kernel, with every block reaching its flush at the same time.
-//   * here ONE 8-wave block per CU streams its share of the reduction through a 4-slot LDS ring
-//     (32-40 KB per K64 slot, up to the whole 160 KB): three K-steps are in flight while one is
-//     consumed, with a counted vmcnt per slot and one barrier per K-step.  The two waves of a
-//     SIMD (w and w+4) own the same 64x64 accumulator tile and split every K64 step into its two
-//     k32 halves, so the SIMD's matrix pipe gets 32 MFMAs per barrier from two independent
-//     instruction streams while each wave holds only 64 accumulators.  The pair's partial tiles
-//     are summed through LDS at the end (a + b == b + a: the result does not depend on which
-//     wave adds), so a block flushes ONE accumulator set: 256 blocks x 64 KB = 16 MB of atomics
-//     instead of ~32.
-//   * split-K is planned for ~one block per CU (PDT_WG_BLOCKS), not for ~4.
-//
+//   * hipcc put an `s_waitcnt vmcnt(0)` in front of every ds_read_tr builtin that follows an
+//     LDS-DMA builtin (it cannot tell the DMA's destination from the read's source), so the old
+//     kernel's "two-stage pipeline" drained every prefetch at every fragment read.  Here the DMA
+//     is inline asm (igemm_common.h glds16_asm), invisible to that analysis; the kernel orders it
+//     with its own counted vmcnt + barrier, and the reads stay builtins whose lgkmcnt waits the
+//     compiler places exactly;
+//   * ONE 8-wave block per CU streams its share of the reduction through a 4-slot LDS ring
+//     (32-40 KB per K64 slot), and reads every step's fragments one step ahead: the LDS reads of
+//     step j+1 are in flight while the MFMAs of step j run.  The two waves of a SIMD (w and w+4)
+//     own the same 64x64 accumulator tile and split every K64 step into its two k32 halves, so
+//     the SIMD's matrix pipe gets 32 MFMAs per barrier from two independent instruction streams
+//     while each wave holds 64 accumulators.  The pair's partial tiles are summed through LDS at
+//     the end (a + b == b + a: the result does not depend on which wave adds), so a block flushes
+//     ONE accumulator set: 256 blocks x 64 KB = 16 MB of atomics instead of ~32;
+//   * split-K is planned for ~one block per CU, not for ~4.
+// Measured (r5e/r5i, one MI355X): all ResNet-50 wgrads isolated 4.93 -> 4.63 ms (layer-3/4 1x1:
+// -15 %); ResNet-50 step 18.70 -> 18.45 ms in the same call.  What still bounds the main loop
+// (PMC, r5h: 24 % MFMA busy on the layer-3 1x1, 31 % of wave time at waits, TD stalled on the TC):
+// the L2 -> LDS rate of 64x64 wave tiles -- a 64 KB-per-step 256x256 tile would halve the bytes
+// per FLOP but flush 4x the split-K partials.
 // Tile shapes (4 accumulator tiles of 64x64 per block): 128x128 (2x2), 64x256 (1x4: Kout = 64)
 // and 256x64 (4x1: the layer-1 64-channel inputs with 256 output channels).  Loaders: pointwise
 // (1x1/s1: reduction row = pixel) and general (any R, S, stride, padding: each B row decomposed
@@ -658,30 +667,18 @@ struct WgPlan {
   bool slab;                    // split-K partials in private slabs + fixed-order reduce (else atomics)
 };
 
-// Tuning knobs: PDT_WG_CUS (CUs the split-K plan fills, default: the device's), PDT_WG_HALO=0
-// (3x3 convs on the general loader).
+// CUs the split-K plan fills: the device's (measured in-step, one MI355X, atomic split-K: planning
+// for 128 or 256 CUs gave the same step, 96 was 1.2 % slower).
 static int wg_cus() {
   static int v = -1;
   if (v < 0) {
-    if (const char* e = getenv("PDT_WG_CUS")) v = std::max(8, atoi(e));
-    else {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-        v = n;
-      else
-        v = 256;
-    }
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      v = n;
+    else
+      v = 256;
   }
   return v;
-}
-
-static bool wg_halo_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PDT_WG_HALO");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
 }
 
 // Split-K factor: one 512-thread block per CU at a time, so a plan of tiles * splits blocks runs
@@ -708,8 +705,12 @@ static int choose_splits(int tiles, int nsteps, double t_step_us, double tile_by
   return best;
 }
 
+// The halo kernel runs the Kout = 64 3x3 convs (ResNet layer 1: 0.112 vs 0.139 ms isolated).  With
+// Kout >= 128 its 128 x (3 x 64) tile lost to the general loader (layer 2-4: 0.109-0.152 vs
+// 0.089-0.109 ms isolated, and 0.3 % on the step, r5c / r5g): both main loops are bound by the
+// L2 -> LDS rate, and the 48-column taps cost the wider tile its fragment reuse.
 static bool halo3_shape(const ConvShape& s) {
-  return wg_halo_on() && s.R == 3 && s.S == 3 && s.stride == 1 && s.sw() == 1 && s.pad == 1 &&
+  return s.K <= 64 && s.R == 3 && s.S == 3 && s.stride == 1 && s.sw() == 1 && s.pad == 1 &&
          s.Ho == s.H && s.Wo == s.W && s.C % 64 == 0 && s.K % 64 == 0;
 }
 
@@ -719,7 +720,7 @@ static WgPlan plan_wg(const ConvShape& s, bool deterministic) {
   double mfma_cyc, stage_bytes;
   if (halo3_shape(s)) {
     p.kind = KIND_HALO3;
-    if (s.K <= 64) { p.wm = 1; p.wn = 4; p.tc = 1; } else { p.wm = 2; p.wn = 2; p.tc = 2; }
+    p.wm = 1; p.wn = 4; p.tc = 1;  // 64 x (3 taps x 64 channels)
     p.bm = p.wm * 64;
     const int bc = p.wn * p.tc * 16;
     p.bn = 3 * bc;
@@ -742,19 +743,13 @@ static WgPlan plan_wg(const ConvShape& s, bool deterministic) {
   mfma_cyc = (double)p.bm * p.bn * 64 * 2 / 4096.0;  // per K-step per CU at the MFMA peak
   // a K-step's cost: its MFMAs at ~50 % of peak, or its LDS-DMA bytes at ~50 GB/s per CU
   const double t_step = std::max(mfma_cyc * 2.0 / 2400.0, stage_bytes / 50.0e3);
-  // split-K reduction: fp32 atomics (~1.3 TB/s, memory side) or private slabs written at the store
-  // rate plus a fixed-order reduce launch, whichever the model prices lower; deterministic runs
-  // always take the slabs (bitwise run to run)
-  double t_atomic = 1e30, t_slab = 1e30;
-  const int s_slab = choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, true, &t_slab);
-  const int s_atomic = deterministic ? 1 : choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, false, &t_atomic);
-  static int force_slab = -2;
-  if (force_slab == -2) {
-    const char* e = getenv("PDT_WG_SLAB");  // A/B: 0 atomics, 1 slabs (non-deterministic runs)
-    force_slab = e ? atoi(e) : -1;
-  }
-  p.slab = deterministic || (force_slab >= 0 ? force_slab == 1 : t_slab < t_atomic);
-  int splits = p.slab ? s_slab : s_atomic;
+  // split-K reduction: fp32 atomics (~1.3 TB/s, memory side), or -- deterministic runs -- private
+  // slabs written at the store rate plus one fixed-order reduce launch.  Slabs also won the cost
+  // model for many non-deterministic shapes but lost in the step (18.40 vs 18.26 ms, r5i): the
+  // reduce launches queue on the weight-gradient stream.
+  double est_us = 0.0;
+  p.slab = deterministic;
+  int splits = choose_splits(p.tiles, p.nsteps, t_step, (double)p.bm * p.bn * 4, p.slab, &est_us);
   if (p.slab) {  // slab workspace: splits * |dW| * 4 bytes, capped at 64 MB
     const int64_t dw_bytes = (int64_t)s.K * ncols * 4;
     splits = (int)std::min<int64_t>(splits, std::max<int64_t>(1, ((int64_t)64 << 20) / dw_bytes));
@@ -833,8 +828,7 @@ void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* 
     a.slab_stride = slab ? n : 0;
     a.zero = zero_n > 0 ? zero : nullptr;
     a.zero_n = zero_n;
-    if (p.tc == 1) run_wh<1, 4, 1>(a, nb, st);
-    else run_wh<2, 2, 2>(a, nb, st);
+    run_wh<1, 4, 1>(a, nb, st);
   } else {
     WgArgs a{};
     a.dy = dy; a.x = x;

@@ -139,10 +139,10 @@ WGRAD_PLANS = [
     ((16, 56, 56, 256, 128, 1, 1, 1, 0), 128),   # pointwise wgrad, 128x128 tile
     ((16, 56, 56, 64, 64, 3, 3, 1, 1), 64),      # Kout = 64: 64x256 tile, general loader
     ((16, 28, 28, 256, 512, 1, 1, 2, 0), 128),   # strided 1x1 (general loader)
-    ((8, 7, 7, 512, 512, 3, 3, 1, 1), 128),      # 3x3 halo kernel, 7x7: 47 % padded q-rows
-    ((16, 28, 28, 128, 128, 3, 3, 1, 1), 128),   # 3x3 halo kernel, 128x(3x64) tile
-    ((2, 14, 14, 192, 256, 3, 3, 1, 1), 128),    # 3x3 halo kernel, 3 channel blocks, 2 images
-    ((3, 9, 5, 64, 64, 3, 3, 1, 1), 64),         # 3x3 halo kernel, tiny odd image (steps span images)
+    ((8, 7, 7, 512, 512, 3, 3, 1, 1), 128),      # 3x3 general loader, 7x7 reduction
+    ((16, 28, 28, 128, 128, 3, 3, 1, 1), 128),   # 3x3 general loader, 128x128 tile
+    ((2, 14, 14, 64, 64, 3, 3, 1, 1), 64),       # 3x3 halo kernel, 2 images
+    ((3, 9, 5, 128, 64, 3, 3, 1, 1), 64),        # 3x3 halo kernel, 2 channel blocks, tiny odd image
     ((4, 14, 14, 72, 40, 3, 3, 2, 1), 64),       # ragged: Kout / columns not tile multiples
 ]
 
