@@ -1352,8 +1352,11 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
 
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(P.dy, P.dy_bytes);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.x, P.x_bytes);
+  // LDS-DMA as asm (igemm_common.h glds16_asm): with the builtin, hipcc drained the prefetched
+  // K-step with an s_waitcnt vmcnt(0) in front of every ds_read_tr8 of the current one
+  const v4i rdy = rsrc_words(P.dy, P.dy_bytes);
+  const v4i rx = rsrc_words(P.x, P.x_bytes);
+  const uint32_t sbase = lds_addr(smem);
 
   // A (dy) lanes: row within the step, source chunk (kout block of 16) that lands in LDS slot
   int a_lane[A_PW];
@@ -1391,12 +1394,12 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
   }
 
   auto issue = [&](int step, int buf) {
-    char* As = smem + buf * STAGE;
-    char* Bs = As + A_BYTES;
+    const uint32_t As = sbase + buf * STAGE;
+    const uint32_t Bs = As + A_BYTES;
     const int mb = step * KS;
     const int abase = mb * P.Kout;
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) glds16(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
+    for (int i = 0; i < A_PW; ++i) glds16_asm(rdy, As + (wid * A_PW + i) * 1024, (uint32_t)(abase + a_lane[i]));
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
       uint32_t off;
@@ -1416,7 +1419,7 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
         b_ho[i] = c2 ? ho - (uint32_t)P.Ho : ho;
         b_n[i] += (uint32_t)P.adv_qn + c2;
       }
-      glds16(rx, Bs + (wid * B_PW + i) * 1024, off);
+      glds16_asm(rx, Bs + (wid * B_PW + i) * 1024, off);
     }
   };
 
@@ -1448,7 +1451,7 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
       for (int j = 0; j < TN; ++j)  // A = dy (e5m2: cbsz 1), B = x (e4m3: blgp 0), unit block scales
         acc[m][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[m], bfr[j], acc[m][j], 1, 0, 0, 0, 0, 0);
     if (i + 1 < nst) wait_vm<0>();
-    lds_barrier();
+    lds_barrier_rd();  // this step's fragment reads retired before the next refill of its buffer
   }
   (void)LPS;
 
