@@ -660,9 +660,44 @@ Tensor bn_finalize(const Tensor& part, int64_t count, const Tensor& rm, const Te
 // Training-mode conv unit forward in ONE host call: conv with BN partial statistics, then the BN
 // finalize (batch mean / invstd / scale / shift, running-stat update).  Saves a Python -> C++
 // round trip per conv unit (155 per ResNet-152 step) over conv_fwd + bn_finalize.
+static pdt::BnFwdFuse bn_fwd_fuse(const Tensor& x, int K, int64_t count, int64_t M, const Tensor& acc,
+                                   const Tensor& rm, const Tensor& rv, const Tensor& gamma,
+                                   const Tensor& beta, double momentum, double eps, Tensor& stats) {
+  TORCH_CHECK(M == count, "conv_fwd_bn: count mismatch");
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.is_contiguous() && acc.numel() >= pdt::kStatSlots * 2 * K &&
+              acc.device() == x.device(), "conv_fwd_bn: acc must be a contiguous fp64 [8][2][K] device tensor");
+  TORCH_CHECK(gamma.scalar_type() == at::kFloat && beta.scalar_type() == at::kFloat && gamma.numel() == K,
+              "BN params must be fp32 [K]");
+  TORCH_CHECK(!rm.defined() || (rm.scalar_type() == at::kFloat && rv.defined() && rm.numel() == K),
+              "running stats must be fp32 [K]");
+  stats = at::empty({4, K}, x.options().dtype(at::kFloat));
+  return pdt::BnFwdFuse{acc.data_ptr<double>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                        rm.defined() ? rm.data_ptr<float>() : nullptr, rv.defined() ? rv.data_ptr<float>() : nullptr,
+                        stats.data_ptr<float>(), (float)momentum, (float)eps};
+}
+
+// acc (fp64 [>= 2K], zero, re-zeroed by the finalize): the conv sums the statistics into it and a
+// one-thread-per-channel finalize reads them (kernels.h BnFwdFuse; fp64 atomics, so not bitwise
+// run-to-run: callers pass it only outside deterministic mode), else the partials + bn_finalize.
 std::tuple<Tensor, Tensor> conv_fwd_bn(const Tensor& x, const Tensor& wk, int64_t stride, int64_t pad,
                                        int64_t count, const Tensor& rm, const Tensor& rv, const Tensor& gamma,
-                                       const Tensor& beta, double momentum, double eps) {
+                                       const Tensor& beta, double momentum, double eps,
+                                       const std::optional<Tensor>& acc) {
+  if (acc.has_value() && acc->defined()) {
+    check_bf16_nhwc(x, "x");
+    check_cuda(wk, "wk");
+    TORCH_CHECK(wk.dim() == 4 && wk.size(3) == x.size(3), "packed weight must be [K,R,S,Cx]");
+    c10::hip::HIPGuard g(x.get_device());
+    auto s = shape_of(x.size(0), x.size(1), x.size(2), x.size(3), wk.size(0), wk.size(1), wk.size(2),
+                      stride, pad);
+    TORCH_CHECK(s.K % 8 == 0, "output channels must be a multiple of 8");
+    auto y = at::empty({s.N, s.Ho, s.Wo, s.K}, x.options());
+    Tensor stats;
+    auto f = bn_fwd_fuse(x, s.K, count, (int64_t)s.N * s.Ho * s.Wo, *acc, rm, rv, gamma, beta, momentum, eps,
+                         stats);
+    pdt::launch_conv_fwd(cbf(x), cbf(wk), bf(y), nullptr, s, cur_stream(x), &f);
+    return {y, stats};
+  }
   auto yp = conv_fwd(x, wk, stride, pad, true);
   Tensor stats = bn_finalize(std::get<1>(yp), count, rm, rv, gamma, beta, momentum, eps, 0);
   return {std::get<0>(yp), stats};
@@ -1238,9 +1273,11 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_fwd_q8(const Tensor& y, const Tensor& 
   return {z, q, zm};
 }
 
+// fp8 forward conv; with `bn` = (count, rm, rv, gamma, beta, momentum, eps, acc) the BN finalize runs
+// inside the conv as in conv_fwd_bn, and the second result is the [4][K] statistics, not partials
 std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const Tensor& oscale,
                                         int64_t stride, int64_t pad, bool stats,
-                                        const std::optional<Tensor>& ascale) {
+                                        const std::optional<Tensor>& ascale, const std::optional<py::tuple>& bn) {
   check_u8_nhwc(x, "x");
   check_cuda(wq, "wq");
   TORCH_CHECK(wq.scalar_type() == at::kByte && wq.dim() == 4 && wq.size(3) == x.size(3),
@@ -1255,7 +1292,14 @@ std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const
   Tensor part;
   float* pp = nullptr;
   int M = s.N * s.Ho * s.Wo;
-  if (stats) {
+  std::optional<pdt::BnFwdFuse> fuse;
+  if (bn.has_value()) {
+    const py::tuple& b = *bn;
+    TORCH_CHECK(b.size() == 8, "bn = (count, rm, rv, gamma, beta, momentum, eps, acc)");
+    auto opt = [](const py::handle& h) { return h.is_none() ? Tensor() : h.cast<Tensor>(); };
+    fuse = bn_fwd_fuse(x, s.K, b[0].cast<int64_t>(), M, b[7].cast<Tensor>(), opt(b[1]), opt(b[2]),
+                       b[3].cast<Tensor>(), b[4].cast<Tensor>(), b[5].cast<double>(), b[6].cast<double>(), part);
+  } else if (stats) {
     int grows = pdt::conv_nt_group_rows(M, s.K, s.R * s.S * s.C);
     part = at::empty({(M + grows - 1) / grows, 2, s.K}, x.options().dtype(at::kFloat));
     pp = part.data_ptr<float>();
@@ -1267,7 +1311,7 @@ std::tuple<Tensor, Tensor> conv_fwd_fp8(const Tensor& x, const Tensor& wq, const
     asp = ascale->data_ptr<float>();
   }
   pdt::launch_conv_fwd_fp8(x.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), oscale.data_ptr<float>(), asp,
-                           bf(y), pp, s, cur_stream(x));
+                           bf(y), pp, s, cur_stream(x), fuse ? &*fuse : nullptr);
   return {y, part};
 }
 
@@ -1333,7 +1377,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
   m.def("conv_fwd_bn", checked("conv_fwd_bn", &conv_fwd_bn), py::arg("x"), py::arg("wk"), py::arg("stride"),
         py::arg("pad"), py::arg("count"), py::arg("rm"), py::arg("rv"), py::arg("gamma"), py::arg("beta"),
-        py::arg("momentum"), py::arg("eps"));
+        py::arg("momentum"), py::arg("eps"), py::arg("acc") = py::none());
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"), py::arg("res_scale") = py::none(),
         py::arg("res_shift") = py::none());
@@ -1379,7 +1423,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("residual"), py::arg("relu"), py::arg("state"), py::arg("slot"),
         py::arg("want_mask") = false, py::arg("want_z") = true);
   m.def("conv_fwd_fp8", checked("conv_fwd_fp8", &conv_fwd_fp8), py::arg("x"), py::arg("wq"), py::arg("oscale"),
-        py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("ascale") = py::none());
+        py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("ascale") = py::none(),
+        py::arg("bn") = py::none());
   m.def("conv_dgrad_fp8", checked("conv_dgrad_fp8", &conv_dgrad_fp8), py::arg("dy8"), py::arg("wt8"),
         py::arg("wscale"), py::arg("ascale"), py::arg("x_shape"), py::arg("stride"), py::arg("pad"),
         py::arg("addend") = py::none());

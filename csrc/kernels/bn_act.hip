@@ -222,6 +222,45 @@ void launch_bn_finalize(const float* part, int ngroups, int grows, int M, int K,
   }
 }
 
+// Finalize from fp64 totals (kernels.h BnFwdFuse): one thread per channel; the sums are read once
+// and re-zeroed for the next conv that accumulates into them.
+__global__ void __launch_bounds__(256) bn_finalize_sums_kernel(double* __restrict__ acc, int M, int K,
+                                                               float* __restrict__ rm, float* __restrict__ rv,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float momentum,
+                                                               float eps, float* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double S = 0.0, Q = 0.0;
+#pragma unroll
+  for (int x = 0; x < kStatSlots; ++x) {  // the conv's per-XCD slots, fixed order
+    double* a = acc + (size_t)x * 2 * K;
+    S += a[k];
+    Q += a[K + k];
+    a[k] = 0.0;
+    a[K + k] = 0.0;
+  }
+  const double Md = (double)M;
+  const double mu = S / Md;
+  const double var = fmax(Q / Md - mu * mu, 0.0);
+  const float invstd = rsqrtf((float)var + eps);
+  if (rm != nullptr) {
+    const float unb = M > 1 ? (float)(var * Md / (Md - 1.0)) : (float)var;
+    rm[k] = (1.f - momentum) * rm[k] + momentum * (float)mu;
+    rv[k] = (1.f - momentum) * rv[k] + momentum * unb;
+  }
+  const float sc = gamma[k] * invstd;
+  out[k] = (float)mu;
+  out[K + k] = invstd;
+  out[2 * K + k] = sc;
+  out[3 * K + k] = beta[k] - (float)mu * sc;
+}
+
+void launch_bn_finalize_sums(const BnFwdFuse& bn, int M, int K, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_sums_kernel, dim3(ceil_div(K, 256)), dim3(256), 0, st, bn.acc, M, K, bn.rm,
+                     bn.rv, bn.gamma, bn.beta, bn.momentum, bn.eps, bn.out);
+}
+
 __global__ void bn_eval_params_kernel(const float* rm, const float* rv, const float* gamma,
                                       const float* beta, float eps, int K, float* out) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;

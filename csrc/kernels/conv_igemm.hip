@@ -114,6 +114,8 @@ struct NtArgs {
   uint32_t halo_bytes;
   FastDiv div_hw2;  // halo pixel -> halo row (divide by WA + 2)
   FastDiv div_ha;   // global image row -> image (divide by HA)
+  // EPI_STATS: non-null -> per-channel fp64 totals of y and y^2 (kernels.h BnFwdFuse) instead of `part`
+  double* sacc;
 };
 
 // epilogue variants of the NT kernel
@@ -248,16 +250,39 @@ constexpr int nt_min_waves() {
 // statistics (EPI_STATS) or the fused BN-backward mask / partial sums (EPI_BNB), bf16 staging
 // through LDS (`smem`, idle pipeline buffers: every wave must be past its last fragment read)
 // and 16-byte row stores.  Every thread of the workgroup calls it (it has block barriers).
-// EPI_STATS: where the BN statistics are summed.  1 (default): in the store loop, from the bf16
-// chunks each lane stores -- the lane's 8 channels are fixed, so a chunk costs 8 unpacks + 4
-// v_pk_add_f32 + 4 v_pk_fma_f32, and one shuffle reduction over the lanes sharing the channels
-// follows.  0: from the fp32 accumulators before staging (one 16-lane DPP row reduction per
-// channel value: ~600 VALU + hazard nops per wave on the 256x256 tile, measured 7.9k cycles per
-// tile with the PDT_NT_TIMING build -- as long as the main loop of a short-K 1x1 conv).  The
-// bf16 statistics are those of the tensor the BN apply reads (torch's autocast semantics).
-#ifndef PDT_STATS_STORE
-#define PDT_STATS_STORE 1
-#endif
+// EPI_STATS: the BN statistics are summed in the store loop, from the bf16 chunks each lane
+// stores -- the lane's 8 channels are fixed, so a chunk costs 8 unpacks + 4 v_pk_add_f32 + 4
+// v_pk_fma_f32, and one shuffle reduction over the lanes sharing the channels follows (summing the
+// fp32 accumulators before staging instead cost ~600 VALU + hazard nops per wave on the 256x256
+// tile, as long as the main loop of a short-K 1x1 conv).  The bf16 statistics are those of the
+// tensor the BN apply reads (torch's autocast semantics).
+
+
+// BN statistics as fp64 totals (NtArgs::sacc), called by every thread of a workgroup after
+// red[WM][2][BN] holds the workgroup's per-channel (sum, sum of squares) by wave row: one
+// fire-and-forget agent-scope fp64 atomic add per channel and moment.  A one-block-per-256-channel
+// launch (launch_bn_finalize_sums) turns the totals into the statistics and re-zeroes them --
+// instead of bn_finalize's reduction over one partial per row tile (3136-6272 of them on layer 1).
+// fp64 totals: var = E[y^2] - mean^2 keeps ~1e-16 relative error where fp32 would cancel.
+template <class CFG, int WM>
+__device__ __forceinline__ void nt_stats_atomic(const NtArgs& P, const float* red, int n0) {
+  constexpr int BN = CFG::BN;
+  const int t = threadIdx.x;
+  const int col = n0 + t;
+  if (t < BN && col < P.Nout) {
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) {
+      S += red[(w * 2 + 0) * BN + t];
+      Q += red[(w * 2 + 1) * BN + t];
+    }
+    // one [2][Nout] slot per XCD (workgroups are dealt to the 8 XCDs round-robin): 8x fewer adds
+    // to each address than one shared total
+    double* slot = P.sacc + (size_t)(blockIdx.x & 7) * 2 * P.Nout;
+    __hip_atomic_fetch_add(slot + col, (double)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(slot + P.Nout + col, (double)Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 template <class CFG, int WM, int WN, int TM, int TN, int EPI, int OP>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN], char* smem, int m0, int n0,
@@ -286,79 +311,6 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
         acc[i][j][0] *= sc.x; acc[i][j][1] *= sc.y; acc[i][j][2] *= sc.z; acc[i][j][3] *= sc.w;
       }
     }
-  }
-
-  if constexpr (EPI == EPI_STATS && !PDT_STATS_STORE) {
-    // one pass: per channel sum and sum of squares over this wave's (<= TM*16) valid pixels,
-    // converted to M2 about the wave's mean (cancellation is benign at <= 64 rows).  The WM wave
-    // rows of the workgroup are then merged in LDS (Chan: M2 = sum M2_w + sum n_w (mean_w -
-    // mean)^2), so ONE partial per (workgroup row tile, channel) goes out and bn_finalize reads
-    // BM-row groups (4x fewer partials on the 256-row tiles than per-wave groups).
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]: the pipeline buffers are idle now
-    const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
-    {
-      const bool full = valid == TM * 16;  // wave-uniform: no per-element masking on full tiles
-      const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float s[4], q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = 0.f, v2 = 0.f;
-          if (full) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-              v += acc[i][j][e];
-              v2 = fmaf(acc[i][j][e], acc[i][j][e], v2);
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-              const float a = (i * 16 + fr < valid) ? acc[i][j][e] : 0.f;
-              v += a;
-              v2 = fmaf(a, a, v2);
-            }
-          }
-          v = row_sum16(v);    // the 16 lanes of a DPP row are the 16 pixels of a tile row
-          v2 = row_sum16(v2);
-          s[e] = v;
-          q[e] = fmaxf(v2 - v * v * inv_valid, 0.f);
-        }
-        if (fr == 0) {
-          const int cl = wn * TN * 16 + j * 16 + fq * 4;  // column within the workgroup tile
-          *reinterpret_cast<float4*>(red + (wm * 2 + 0) * BN + cl) = make_float4(s[0], s[1], s[2], s[3]);
-          *reinterpret_cast<float4*>(red + (wm * 2 + 1) * BN + cl) = make_float4(q[0], q[1], q[2], q[3]);
-        }
-      }
-    }
-    __syncthreads();
-    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
-      float sw[WM], qw[WM], nw[WM];
-      float S = 0.f, Nr = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        nw[w] = (float)max(0, min(TM * 16, P.M - (m0 + w * TM * 16)));
-        sw[w] = red[(w * 2 + 0) * BN + t];
-        qw[w] = red[(w * 2 + 1) * BN + t];
-        S += sw[w];
-        Nr += nw[w];
-      }
-      const float mean = S / Nr;  // Nr > 0: the tile's first wave row is inside the GEMM
-      float Q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        if (nw[w] > 0.f) {
-          const float d = sw[w] / nw[w] - mean;
-          Q += qw[w] + nw[w] * d * d;
-        }
-      }
-      const int col = n0 + t;
-      if (col < P.Nout) {
-        P.part[((int64_t)tmi * 2 + 0) * P.Nout + col] = S;
-        P.part[((int64_t)tmi * 2 + 1) * P.Nout + col] = Q;
-      }
-    }
-    __syncthreads();  // red[] aliases the staging rows written next
   }
 
   NT_STAMP(3);
@@ -537,7 +489,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
             bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
           }
         }
-        if constexpr (EPI == EPI_STATS && PDT_STATS_STORE) {
+        if constexpr (EPI == EPI_STATS) {
           // rows past the GEMM edge were staged as 0 (their accumulators are 0): no mask needed
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
@@ -573,7 +525,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   } else {
     if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{});
   }
-  if constexpr (EPI == EPI_STATS && PDT_STATS_STORE) {
+  if constexpr (EPI == EPI_STATS) {
     float s8[8], q8[8];
 #pragma unroll
     for (int h = 0; h < 4; ++h) { s8[2 * h] = st_s[h].x; s8[2 * h + 1] = st_s[h].y; q8[2 * h] = st_q[h].x; q8[2 * h + 1] = st_q[h].y; }
@@ -585,8 +537,10 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
         s8[q] += __shfl_xor(s8[q], o, 64);
         q8[q] += __shfl_xor(q8[q], o, 64);
       }
-    // M2 about the wave's mean (cancellation benign at <= 64 rows), then the WM wave rows of the
-    // workgroup merge in LDS (Chan) into ONE partial per (row tile, channel), as bn_finalize reads
+    const bool fused = P.sacc != nullptr;
+    // partials path: M2 about the wave's mean (cancellation benign at <= 64 rows), then the WM wave
+    // rows of the workgroup merge in LDS (Chan) into ONE partial per (row tile, channel), as
+    // bn_finalize reads.  Fused path: plain sums and sums of squares, added to fp64 totals.
     const int valid = min(TM * 16, P.M - wrow0);  // <= 0: wave past the GEMM edge, contributes 0
     const float inv_valid = valid > 0 ? 1.f / (float)valid : 0.f;
     __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
@@ -594,7 +548,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
     if (lane < CH_PER_ROW) {
       float m2[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) m2[q] = fmaxf(q8[q] - s8[q] * s8[q] * inv_valid, 0.f);
+      for (int q = 0; q < 8; ++q) m2[q] = fused ? q8[q] : fmaxf(q8[q] - s8[q] * s8[q] * inv_valid, 0.f);
       float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
       *reinterpret_cast<float4*>(rp) = make_float4(s8[0], s8[1], s8[2], s8[3]);
       *reinterpret_cast<float4*>(rp + 4) = make_float4(s8[4], s8[5], s8[6], s8[7]);
@@ -602,7 +556,9 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
       *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(m2[4], m2[5], m2[6], m2[7]);
     }
     __syncthreads();
-    if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
+    if (fused) {
+      nt_stats_atomic<CFG, WM>(P, red, n0);
+    } else if (t < BN) {  // thread t merges channel n0 + t over the WM wave rows (fixed order)
       float sw[WM], qw[WM], nw[WM];
       float S = 0.f, Nr = 0.f;
 #pragma unroll
@@ -1697,9 +1653,10 @@ static void fill_common(NtArgs& a, int Mi, int Mj) {
 }
 
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
-                     const ConvShape& s, hipStream_t st) {
+                     const ConvShape& s, hipStream_t st, const BnFwdFuse* bn) {
   NtArgs a{};
   a.a = x; a.b = w; a.out = y; a.part = part;
+  if (bn != nullptr) { a.sacc = bn->acc; a.part = nullptr; }
   a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C * 2);
   a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C * 2);
   a.o_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
@@ -1720,21 +1677,23 @@ void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* p
     a.c8_rows = 8 / s.S;
     a.c8_step = a.c8_rows * s.W * 8 * 2;
   }
-  if (part) {
+  if (part || bn) {
     if (c64) dispatch_nt<true, EPI_STATS>(a, st);
     else dispatch_nt<false, EPI_STATS>(a, st);
   } else {
     if (c64) dispatch_nt<true, EPI_PLAIN>(a, st);
     else dispatch_nt<false, EPI_PLAIN>(a, st);
   }
+  if (bn != nullptr) launch_bn_finalize_sums(*bn, a.M, s.K, st);
 }
 
 void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, const float* ascale,
-                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st) {
+                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st, const BnFwdFuse* bn) {
   if (s.C % 16 != 0) throw std::runtime_error("conv_fwd_fp8: input channels must be a multiple of 16");
   NtArgs a{};
   a.a = reinterpret_cast<const uint16_t*>(x); a.b = reinterpret_cast<const uint16_t*>(w);
   a.out = y; a.part = part; a.oscale = oscale; a.ascale = ascale;
+  if (bn != nullptr) { a.sacc = bn->acc; a.part = nullptr; }
   a.a_bytes = (uint32_t)((int64_t)s.N * s.H * s.W * s.C);
   a.b_bytes = (uint32_t)((int64_t)s.K * s.R * s.S * s.C);
   a.o_bytes = (uint32_t)((int64_t)s.N * s.Ho * s.Wo * s.K * 2);
@@ -1749,13 +1708,14 @@ void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale
   a.tr0 = 0; a.ts0 = 0; a.tstep = 1;
   a.dr0 = 0; a.ds0 = 0; a.dstep = 1;
   const bool c128 = (s.C % 128) == 0 && s.R * s.S <= 32;
-  if (part) {
+  if (part || bn) {
     if (c128) dispatch_nt<true, EPI_STATS, OP_F8_E4M3>(a, st);
     else dispatch_nt<false, EPI_STATS, OP_F8_E4M3>(a, st);
   } else {
     if (c128) dispatch_nt<true, EPI_PLAIN, OP_F8_E4M3>(a, st);
     else dispatch_nt<false, EPI_PLAIN, OP_F8_E4M3>(a, st);
   }
+  if (bn != nullptr) launch_bn_finalize_sums(*bn, a.M, s.K, st);
 }
 
 static int dgrad_class_rows(const ConvShape& s, int ph, int pw) {

@@ -74,8 +74,23 @@ void conv_nt_force(int k32, int mid);
 // (s_memtime at start / first operands in LDS / main loop done / epilogue stats done / end, plus
 // s_memrealtime and the CU id), 8 values per block id, copied into `host`; other builds return 0.
 int nt_timing_fetch(unsigned long long* host, int n);
+// BatchNorm statistics as fp64 totals (non-deterministic training runs): every workgroup of the
+// forward conv adds its per-channel sum and sum of squares of the bf16 output to acc[2][K] (agent-
+// scope atomics, no partials buffer); then launch_bn_finalize_sums (one thread per channel) turns
+// them into out[4][K] (mean, invstd, scale, shift), updates the running statistics and re-zeroes acc.
+constexpr int kStatSlots = 8;  // acc slots: one per XCD
+struct BnFwdFuse {
+  double* acc;           // [kStatSlots][2][K], zero on entry, zero again on exit
+  const float* gamma;
+  const float* beta;
+  float* rm;             // running mean / var, or null
+  float* rv;
+  float* out;            // [4][K]
+  float momentum, eps;
+};
+void launch_bn_finalize_sums(const BnFwdFuse& bn, int M, int K, hipStream_t st);
 void launch_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
-                     const ConvShape& s, hipStream_t st);
+                     const ConvShape& s, hipStream_t st, const BnFwdFuse* bn = nullptr);
 // dx[N,H,W,C] = dgrad(dy[N,Ho,Wo,K], wt[C][R][S][K]) (+ addend[N,H,W,C] if non-null);
 // all stride/pad combos (stride > 1 as stride^2 parity classes)
 // Optional fused BatchNorm backward of the unit whose output x was (dx = dL/dx of that unit's
@@ -261,7 +276,8 @@ size_t quant_rows_entry_bytes();
 // fp8 forward conv: x e4m3 NHWC (C % 16 == 0), w e4m3 [K][R][S][C],
 // y bf16 = (x*w) * oscale[k] * (ascale ? ascale[0] : 1)
 void launch_conv_fwd_fp8(const uint8_t* x, const uint8_t* w, const float* oscale, const float* ascale,
-                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st);
+                         uint16_t* y, float* part, const ConvShape& s, hipStream_t st,
+                         const BnFwdFuse* bn = nullptr);
 // fp8 dgrad: dy e5m2 NHWC (K % 128 == 0), wt e4m3 [C][R][S][K] with per-C scale oscale[c],
 // activation (dy) dequant factor ascale[0]; otherwise as launch_conv_dgrad
 void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,

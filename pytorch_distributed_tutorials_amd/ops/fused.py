@@ -58,6 +58,19 @@ def _bacc(p, c):
         a = torch.zeros(2, c, dtype=torch.float32, device=p.device)
         p._pdt_bacc = a
     return a
+
+
+def _facc(p, c):
+    """The zeroed fp64 [8, 2, C] forward BN-sum accumulator of BatchNorm weight ``p``: the conv
+    producing the BN input adds its per-channel sums into it (one slot per XCD) and the finalize
+    that reads them re-zeroes it (kernels.h BnFwdFuse)."""
+    a = getattr(p, "_pdt_facc", None)
+    if a is None or a.numel() != 16 * c or a.device != p.device:
+        a = torch.zeros(8, 2, c, dtype=torch.float64, device=p.device)  # one slot per XCD
+        p._pdt_facc = a
+    return a
+
+
 _FUSE_RES_BN = True  # shortcut BN applied in the block tail
 # test hook (tests/test_blocks_gpu.py, mask-matched reference): when a list, every fused block
 # forward appends its units' stored post-activation outputs (z, NHWC bf16), so an fp32 reference
@@ -211,15 +224,18 @@ class _ConvBN(torch.autograd.Function):
         if x.is_cuda:
             C = native()
             wk = C.pack_weight(weight, cx)                       # bf16 [K,R,S,Cx]
-            y, part = C.conv_fwd(x, wk, stride, pad, training)    # bf16 NHWC + tile stats
-            buffers_ready()
             if training:
+                buffers_ready()
                 if running_mean is None:  # track_running_stats=False: updates go to scratch
                     running_mean = torch.zeros(k, device=x.device)
                     running_var = torch.ones(k, device=x.device)
-                stats = C.bn_finalize(part, count, running_mean, running_var,
-                                      gamma, beta, float(momentum), float(eps))
+                # the fused block's conv + statistics call (same kernels, same rounding)
+                y, stats = C.conv_fwd_bn(x, wk, stride, pad, count, running_mean, running_var, gamma, beta,
+                                         float(momentum), float(eps),
+                                         None if deterministic() else _facc(gamma, k))
             else:
+                y, _ = C.conv_fwd(x, wk, stride, pad, False)
+                buffers_ready()
                 stats = C.bn_eval_params(running_mean, running_var, gamma, beta, float(eps))
             mean, invstd, scale, shift = stats.unbind(0)
             z = C.bn_act_fwd(y, scale, shift, residual, relu)
@@ -799,9 +815,14 @@ def _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, moment
         # conv + BN finalize in one host call (the running-stat update waits for the buffers first)
         buffers_ready()
         return C.conv_fwd_bn(x, _packed_krsc(C, w, cx), stride, pad, count, rm, rv, gamma, beta,
-                             float(momentum), float(eps))
+                             float(momentum), float(eps), None if deterministic() else _facc(gamma, w.shape[0]))
     if x8 is not None:
         wq, wsc = _packed_krsc8(C, w, cx)
+        if training and not _NAN_TRACE and not deterministic():
+            # BN finalize inside the conv (conv_fwd_bn's fused path)
+            buffers_ready()
+            return C.conv_fwd_fp8(x8[0], wq, wsc, stride, pad, True, x8[1],
+                                  (count, rm, rv, gamma, beta, float(momentum), float(eps), _facc(gamma, k)))
         y, part = C.conv_fwd_fp8(x8[0], wq, wsc, stride, pad, training, x8[1])
     else:
         wk = _packed_krsc(C, w, cx)

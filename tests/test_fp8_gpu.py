@@ -173,6 +173,15 @@ def test_conv_fwd_fp8(gpu, native_ext, shape):
                           torch.ones(k, device=gpu), torch.zeros(k, device=gpu), 0.1, 1e-5)
     mean_r, _ = ref.bn_batch_stats(yr)
     assert torch.allclose(stats[0], mean_r, atol=5e-3, rtol=2e-2)
+    # the same conv with the BN finalize fused (fp64 sums, last workgroup per channel tile)
+    acc = torch.zeros(8, 2, k, dtype=torch.float64, device=gpu)
+    rm, rv = torch.zeros(k, device=gpu), torch.ones(k, device=gpu)
+    ones, zeros = torch.ones(k, device=gpu), torch.zeros(k, device=gpu)
+    y2, st2 = C.conv_fwd_fp8(xq, wq, osc, st, pd, True, None,
+                             (yr.numel() // k, rm, rv, ones, zeros, 0.1, 1e-5, acc))
+    assert torch.equal(y2, y)
+    assert torch.allclose(st2, stats, rtol=2e-4, atol=1e-5)
+    assert torch.count_nonzero(acc) == 0
 
 
 def test_bn_act_fwd_q8_matches_bf16_apply(gpu, native_ext):

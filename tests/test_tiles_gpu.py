@@ -78,6 +78,47 @@ def test_fwd_stats_per_tile(gpu, native_ext, shape, tile):
     assert torch.allclose(stats[1], torch.rsqrt(var_r + 1e-5), rtol=2e-2)
 
 
+@pytest.mark.parametrize("shape,tile", FWD_TILES + [((3, 9, 7, 64, 72, 3, 3, 1, 1), (64, 128))])
+def test_fwd_bn_fused_finalize_matches_partials(gpu, native_ext, shape, tile):
+    """conv_fwd_bn with an fp64 accumulator (per-XCD slots of per-channel sums added by every
+    workgroup, then a one-thread-per-channel finalize) vs the partials + bn_finalize path: same y
+    bitwise, statistics and running-stat update within fp32 rounding, the accumulator back to
+    zero, and a second call (on another stream) agrees too."""
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    x, wt, _ = _operands(shape, gpu, 3)
+    ho = (h + 2 * pd - r) // st + 1
+    wo = (w + 2 * pd - s) // st + 1
+    M = n * ho * wo
+    wk = C.pack_weight(wt, c)
+    g = torch.Generator().manual_seed(5)
+    gamma = (1 + 0.1 * torch.randn(k, generator=g)).to(gpu)
+    beta = (0.1 * torch.randn(k, generator=g)).to(gpu)
+    rm0 = (0.1 * torch.randn(k, generator=g)).to(gpu)
+    rv0 = (1 + 0.1 * torch.rand(k, generator=g)).to(gpu)
+    rm_a, rv_a = rm0.clone(), rv0.clone()
+    y_a, st_a = C.conv_fwd_bn(x, wk, st, pd, M, rm_a, rv_a, gamma, beta, 0.1, 1e-5)
+    acc = torch.zeros(8, 2, k, dtype=torch.float64, device=gpu)
+    for rep in range(2):
+        rm_b, rv_b = rm0.clone(), rv0.clone()
+        side = torch.cuda.Stream() if rep == 1 else torch.cuda.current_stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            y_b, st_b = C.conv_fwd_bn(x, wk, st, pd, M, rm_b, rv_b, gamma, beta, 0.1, 1e-5, acc)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        assert torch.equal(y_a, y_b)
+        assert torch.allclose(st_b, st_a, rtol=2e-4, atol=1e-5), (st_b - st_a).abs().max()
+        assert torch.allclose(rm_b, rm_a, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(rv_b, rv_a, rtol=2e-4, atol=1e-6)
+        assert torch.count_nonzero(acc) == 0
+    yr = ref.conv2d_nhwc(x, wt, st, pd)
+    mean_r, var_r = ref.bn_batch_stats(y_b.float())
+    assert torch.allclose(st_b[0], mean_r, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(st_b[1], torch.rsqrt(var_r + 1e-5), rtol=1e-4)
+    assert _rel(y_b, yr) < 1e-2
+
+
 # dgrad GEMM (per parity class): M = N*H*W / stride^2, Nout = C, K_gemm = R*S*K
 DGRAD_TILES = [
     ((16, 56, 56, 256, 128, 1, 1, 1, 0), (128, 256)),   # short-K (K = 128): the 128x256 tile
