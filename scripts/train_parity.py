@@ -60,10 +60,17 @@ def main():
     ap.add_argument("--classes", type=int, default=10)
     ap.add_argument("--fp8", action="store_true",
                     help="native side on the fp8 path (e4m3 activations / e5m2 gradients, fp8 wgrad)")
+    ap.add_argument("--fp8-parts", default="all", choices=["all", "fwd", "fwd+dgrad"],
+                    help="diagnostics: which GEMMs take fp8 (forward only / + input gradients / + weight "
+                         "gradients)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.fp8:
         ops.set_fp8(True)
+        from pytorch_distributed_tutorials_amd.ops import fused
+        fused._FP8_BWD = a.fp8_parts != "fwd"
+        fused._FP8_WGRAD = a.fp8_parts == "all"
+        fused._FP8_ONLY = a.fp8_parts == "all" 
     ds = learnable_dataset(a.samples, a.image, a.classes, device=dev, seed=3, noise=a.noise)
     torch.manual_seed(0)
     stock = build_model(a.arch, num_classes=a.classes).to(dev)
@@ -97,7 +104,7 @@ def main():
     w = a.window
     nwin = a.steps // w
     res = {
-        "arch": a.arch, "image": a.image, "fp8": bool(a.fp8),
+        "arch": a.arch, "image": a.image, "fp8": bool(a.fp8), "fp8_parts": a.fp8_parts if a.fp8 else None,
         "steps": a.steps, "batch": a.batch, "samples": a.samples, "noise": a.noise, "lr": a.lr,
         "window": w,
         "native_window_loss": [round(float(ln[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],

@@ -81,16 +81,11 @@ def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
     # both learn (the loss falls well below its start), and track each other window by window
     assert n[-1] < 0.2 * n[0] and s[-1] < 0.2 * s[0], (n, s)
     assert res["native_train_acc"] > 0.9 and res["stock_train_acc"] > 0.9, res
-    # fp8: the steepest part of the curve (windows 4-6) is where e4m3 activations / e5m2 gradients
-    # shift the descent by up to ~20 steps, and the fp8 weight gradients accumulate with atomics
-    # (not bitwise reproducible): r4 runs of the same config gave window 5 = 1.71 / 1.48 / 1.81
-    # and window 6 = 1.49 (stock 1.25 / 0.85), each ending at the stock loss and accuracy.  So the
-    # fp8 curve must stay within a wider band of the stock curve at the same window or at most ONE
-    # window (20 steps) later; bf16 keeps the ResNet-18 criterion (same window, 0.15 + 25 %).
-    if fp8:
-        band = lambda b: 0.25 + 0.35 * b  # noqa: E731
-        for i, a in enumerate(n):
-            assert any(abs(a - s[j]) <= band(s[j]) for j in (i - 1, i) if j >= 0), (i, n, s)
-    else:
-        for a, b in zip(n, s):
-            assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)
+    # fp8 and bf16: the same criterion as ResNet-18 -- every 20-step window within 0.15 + 25 % of
+    # the stock curve AT THE SAME WINDOW, and the final accuracy above 0.95.  (Round 4 allowed fp8
+    # a one-window lag; it does not reproduce at round-5 HEAD: profiles/r6_fp8_parity.txt has 4 fp8
+    # and 2 bf16 runs, all inside the same-window band, and per-part runs showing no GEMM family
+    # lagging systematically -- the steep windows move by up to ~0.4 run to run in bf16 too.)
+    assert res["native_train_acc"] > 0.95, res
+    for a, b in zip(n, s):
+        assert abs(a - b) <= 0.15 + 0.25 * b, (n, s)
