@@ -299,6 +299,80 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
                        });
 }
 
+// Folded BN backward (kernels.h DgradFold): (wfold [C][K + C] bf16, bias [C] fp32) for the 1x1 conv
+// whose transposed bf16 weights are wt [C][K] (or [C][1][1][K]), from its output BN's statistics,
+// gamma and backward sums over `count` rows.
+std::tuple<Tensor, Tensor> bn_fold_weights(const Tensor& wt, const Tensor& stats, const Tensor& gamma,
+                                           const Tensor& sums, int64_t count) {
+  check_cuda(wt, "wt");
+  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() == wt.size(0) * wt.size(-1),
+              "wt must be contiguous bf16 [C][K]");
+  const int C = wt.size(0), K = wt.size(-1);
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == 4 * K, "stats: fp32 [4, K]");
+  TORCH_CHECK(gamma.scalar_type() == at::kFloat && gamma.numel() == K, "gamma: fp32 [K]");
+  TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous() && sums.numel() == 2 * K, "sums: fp32 [2, K]");
+  c10::hip::HIPGuard g(wt.get_device());
+  auto wfold = at::empty({C, K + C}, wt.options());
+  auto bias_ws = at::empty({C + 2 * K}, stats.options());  // bias, then the kernel's coefficient scratch
+  auto bias = bias_ws.narrow(0, 0, C);
+  pdt::launch_bn_fold_weights(reinterpret_cast<const uint16_t*>(wt.data_ptr()), stats.data_ptr<float>(),
+                              gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K,
+                              reinterpret_cast<uint16_t*>(wfold.data_ptr()), bias.data_ptr<float>(), cur_stream(wt));
+  return {wfold, bias};
+}
+
+static std::pair<float*, float*> bn_param_sinks(const std::optional<Tensor>& dgamma,
+                                                const std::optional<Tensor>& dbeta, int64_t K);
+
+// Weight gradient of a folded unit (kernels.h launch_bn_fold_wgrad): out [K,C,1,1] fp32 (a KRSC-dense
+// view, e.g. the flat gradient buffer) += diag(k1) t1 + diag(a) w gram + b colsum^T; dgamma/dbeta
+// (optional) take the BN parameter gradients.
+void bn_fold_wgrad(const Tensor& t1, const Tensor& gram, const Tensor& colsum, const Tensor& w,
+                   const Tensor& stats, const Tensor& gamma, const Tensor& sums, int64_t count, Tensor out,
+                   const std::optional<Tensor>& dgamma, const std::optional<Tensor>& dbeta) {
+  const int K = w.size(0), C = w.size(1);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == (int64_t)K * C, "w: fp32 [K, C, 1, 1]");
+  TORCH_CHECK(t1.scalar_type() == at::kFloat && t1.numel() == (int64_t)K * C, "t1: fp32 [K, C]");
+  TORCH_CHECK(gram.scalar_type() == at::kFloat && gram.numel() == (int64_t)C * C, "gram: fp32 [C, C]");
+  TORCH_CHECK(colsum.scalar_type() == at::kFloat && colsum.numel() >= C && colsum.is_contiguous(), "colsum: fp32 [C]");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == (int64_t)K * C, "out: fp32 [K, C, 1, 1]");
+  for (const Tensor* x : {&t1, &gram, &w, const_cast<const Tensor*>(&out)}) {
+    // 1x1: [K,C,1,1] in either memory format is [K][C] memory when its two big strides are (C, 1)
+    TORCH_CHECK(x->stride(0) == x->size(1) && x->stride(1) == 1, "fold wgrad: [K][C]-dense operands");
+  }
+  TORCH_CHECK(stats.numel() == 4 * K && gamma.numel() == K && sums.numel() == 2 * K, "BN operands: [4,K], [K], [2,K]");
+  c10::hip::HIPGuard g(w.get_device());
+  auto pg = bn_param_sinks(dgamma, dbeta, K);
+  pdt::launch_bn_fold_wgrad(t1.data_ptr<float>(), gram.data_ptr<float>(), colsum.data_ptr<float>(), w.data_ptr<float>(),
+                            stats.data_ptr<float>(), gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K,
+                            out.data_ptr<float>(), pg.first, pg.second, cur_stream(w));
+}
+
+// BN-fused dgrad of a 1x1 / stride-1 conv with the NEXT unit's BN backward folded in (kernels.h
+// DgradFold): dx = [g | z] x wfold^T + bias, then the usual BN-fused epilogue (mask, sums into acc).
+// g [N,H,W,K] is that BN's masked gradient, z [N,H,W,C] the conv's input; acc mode only.
+std::tuple<Tensor, Tensor> conv_dgrad_bn_fold(const Tensor& g, const Tensor& z_in, const Tensor& wfold,
+                                              const Tensor& bias, const Tensor& y, const std::optional<Tensor>& z,
+                                              const Tensor& stats, int64_t mask, const Tensor& acc) {
+  check_bf16_nhwc(g, "g");
+  check_bf16_nhwc(z_in, "z_in");
+  const int K = g.size(3), C = z_in.size(3);
+  TORCH_CHECK(z_in.size(0) == g.size(0) && z_in.size(1) == g.size(1) && z_in.size(2) == g.size(2),
+              "fold: g and z must share N, H, W");
+  TORCH_CHECK(wfold.scalar_type() == at::kBFloat16 && wfold.is_contiguous() && wfold.size(0) == C &&
+              wfold.size(1) == K + C, "wfold must be bf16 [C][K + C]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == C, "bias: fp32 [C]");
+  c10::hip::HIPGuard gd(g.get_device());
+  auto s = shape_of(g.size(0), g.size(1), g.size(2), C, K, 1, 1, 1, 0);
+  pdt::DgradFold fold{cbf(z_in), C, bias.data_ptr<float>()};
+  return dgrad_bn_core(g, s, std::nullopt, y, z, stats, mask, std::nullopt, std::nullopt, acc,
+                       [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
+                           hipStream_t st, int asub) {
+                         pdt::launch_conv_dgrad(cbf(g), reinterpret_cast<const uint16_t*>(wfold.data_ptr()), dx,
+                                                ap, sh, st, bn, asub, &fold);
+                       });
+}
+
 // fp8 dgrad operands: dy8 e5m2 NHWC [N,Ho,Wo,K], wt8 e4m3 [C,R,S,K] with per-C scale wscale,
 // dy dequant factor ascale (device scalar)
 pdt::ConvShape fp8_dgrad_shape(const Tensor& dy8, const Tensor& wt8, const Tensor& wscale, const Tensor& ascale,
@@ -478,6 +552,14 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
     st = sst.stream();
   }
   Tensor r;
+  // a consumed BN-sum accumulator: the kernel's workgroup 0 clears it (as conv_wgrad_side)
+  float* zp = nullptr;
+  int zn = 0;
+  if (zero.has_value() && zero->defined()) {
+    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous(), "zero: contiguous fp32");
+    zp = zero->data_ptr<float>();
+    zn = (int)zero->numel();
+  }
   if (out.has_value() && out->defined()) {
     const Tensor& o = *out;
     TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
@@ -486,16 +568,14 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
     for (int d = 0; d < 4; ++d)
       TORCH_CHECK(o.size(d) == 1 || o.stride(d) == want[d], "wgrad out must be channels_last (KRSC) dense");
     pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
-                               x_deq.data_ptr<float>(), o.data_ptr<float>(), s, true, st);
+                               x_deq.data_ptr<float>(), o.data_ptr<float>(), s, true, st, zp, zn);
     r = o;
   } else {
     auto dwp = at::empty({K, R, S, C}, x8.options().dtype(at::kFloat));
     pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
-                               x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st);
+                               x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st, zp, zn);
     r = dwp.permute({0, 3, 1, 2});
   }
-  if (zero.has_value() && zero->defined())  // as conv_wgrad_side: a consumed BN-sum accumulator
-    TORCH_CHECK(hipMemsetAsync(zero->data_ptr(), 0, zero->nbytes(), st) == hipSuccess, "memset");
   if (side != 0) {
     auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
     for (const Tensor* t : {&dy8, &x8, &dy_deq, &x_deq})
@@ -1375,6 +1455,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rv"), py::arg("gamma"), py::arg("beta"), py::arg("momentum"), py::arg("eps"),
         py::arg("grows") = 0);
   m.def("bn_eval_params", checked("bn_eval_params", &bn_eval_params));
+  m.def("bn_fold_weights", checked("bn_fold_weights", &bn_fold_weights), py::arg("wt"), py::arg("stats"),
+        py::arg("gamma"), py::arg("sums"), py::arg("count"));
+  m.def("bn_fold_wgrad", checked("bn_fold_wgrad", &bn_fold_wgrad), py::arg("t1"), py::arg("gram"),
+        py::arg("colsum"), py::arg("w"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("count"),
+        py::arg("out"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+  m.def("conv_dgrad_bn_fold", checked("conv_dgrad_bn_fold", &conv_dgrad_bn_fold), py::arg("g"), py::arg("z_in"),
+        py::arg("wfold"), py::arg("bias"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
+        py::arg("acc"));
   m.def("conv_fwd_bn", checked("conv_fwd_bn", &conv_fwd_bn), py::arg("x"), py::arg("wk"), py::arg("stride"),
         py::arg("pad"), py::arg("count"), py::arg("rm"), py::arg("rv"), py::arg("gamma"), py::arg("beta"),
         py::arg("momentum"), py::arg("eps"), py::arg("acc") = py::none());
@@ -1448,7 +1536,7 @@ PYBIND11_MODULE(_C, m) {
     const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
     return out.narrow(0, 0, got);
   }, py::arg("n"));
-  m.def("conv_nt_force", &pdt::conv_nt_force, py::arg("k32") = -1, py::arg("mid") = -1);
+  m.def("conv_nt_force", &pdt::conv_nt_force, py::arg("k32") = -1, py::arg("mid") = -1, py::arg("wide") = -1);
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);

@@ -20,6 +20,12 @@
 
 namespace pdt {
 
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // ------------------------------------------------------------------ finalize
 // Group g (grows rows, the last one possibly fewer) carries (s_g, q_g) = (sum, M2 about its mean).
 // With S = sum s_g, A = sum q_g, B = sum s_g^2/n_g:  mean = S/M,  M2 = A + B - S^2/M
@@ -261,6 +267,230 @@ void launch_bn_finalize_sums(const BnFwdFuse& bn, int M, int K, hipStream_t st) 
                      bn.rv, bn.gamma, bn.beta, bn.momentum, bn.eps, bn.out);
 }
 
+// ------------------------------------------------------------ folded BN backward
+// DgradFold weights (kernels.h).  Per output channel k of the 1x1 conv (K of them), from its BN
+// statistics and backward sums over M rows:
+//   k1 = gamma * invstd,  k2 = s1 * invstd^2 / M,  a = -k1 * k2,  b = -k1 * (s0 / M - mean * k2)
+// so that the BN-backward apply is dy = k1*g + a*y + b.  With wt[C][K] the transposed weights:
+//   wfold[c][0:K]   = bf16(wt[c][k] * k1[k])
+//   wfold[c][K + c'] = bf16(G[c][c']),  G = sum_k wt[c][k] * a[k] * wt[c'][k]   (fp32 sums)
+//   bias[c]        = sum_k wt[c][k] * b[k]
+// One launch: blocks [0, nG) compute 32x32 tiles of G (the tj == 0 column of tiles also the bias of
+// their 32 rows), the other nS blocks scale wt.  a[] and b[] are built once per block in LDS; the
+// K loop prefetches the next 64-wide chunk into registers while the current one is multiplied.
+struct FoldCoef {
+  const float* stats;
+  const float* gamma;
+  const float* sums;
+  int K;
+  float invM;
+  __device__ __forceinline__ void ab(int k, float& a, float& b) const {
+    const float is = stats[K + k], mu = stats[k];
+    const float k1 = gamma[k] * is;
+    const float k2 = sums[K + k] * is * is * invM;
+    a = -k1 * k2;
+    b = -k1 * (sums[k] * invM - mu * k2);
+  }
+};
+
+constexpr int kFoldMaxK = 2048;
+typedef __bf16 fold_v8bf __attribute__((ext_vector_type(8)));
+
+// Per-channel coefficients (a, b) of the fold into coef[2][K]: its own tiny launch so that the
+// GEMM below needs no LDS -- both then fit on CUs whose LDS the weight-gradient blocks of the side
+// stream hold (a kernel that needs LDS waits for one of those long-lived blocks to retire: the
+// 16-KB-LDS version of this kernel measured 38 us per call in-step against ~5 us of work).
+__global__ void __launch_bounds__(256) bn_fold_coef_kernel(FoldCoef cf, float* __restrict__ coef) {
+  __builtin_amdgcn_s_setprio(3);
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < cf.K) cf.ab(k, coef[k], coef[cf.K + k]);
+}
+
+// G tiles on the matrix cores: a 4-wave workgroup per 32 x 32 tile, wave w taking the K quarter w
+// (4 waves per CU hide the fragment-load latency the one-wave form was bound by: 38 us at C = 512),
+// partial tiles summed through 12 KB of LDS.  Each wave runs K/64 v_mfma_f32_32x32x16_bf16 with
+// A = (wt rows c) * a and B = wt rows c', fragments straight from global memory one 64-k batch
+// ahead.  Lane l: fragment row l & 31, k = 8 * (l >> 5) .. +7 of each 16-k step; accumulator
+// element e: column l & 31, row 8 * (e >> 2) + 4 * (l >> 5) + (e & 3) (G is symmetric, so a
+// transposed tile would read the same).  Waves of the first column of tiles also form the bias.
+__global__ void __launch_bounds__(256) bn_fold_weights_kernel(const uint16_t* __restrict__ wt, FoldCoef cf,
+                                                              const float* __restrict__ coef, int C, int nG,
+                                                              uint16_t* __restrict__ wfold,
+                                                              float* __restrict__ bias) {
+  // on the critical stream, sharing SIMDs with the side stream's weight-gradient waves: ask for
+  // issue priority over them
+  __builtin_amdgcn_s_setprio(3);
+  const int K = cf.K, t = threadIdx.x;
+  const int KC = K + C;
+  const int bid = blockIdx.x;
+  if (bid >= nG) {  // scaled weights: 8 consecutive k of one row per thread
+    const int64_t e = ((int64_t)(bid - nG) * 256 + t) * 8;
+    if (e >= (int64_t)C * K) return;
+    const int c = (int)(e / K), k = (int)(e - (int64_t)c * K);
+    f8 v = unpack8(*reinterpret_cast<const uint4*>(wt + e));
+    float g8[8], i8[8];
+    load8(cf.gamma + k, g8);
+    load8(cf.stats + K + k, i8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v.v[q] *= g8[q] * i8[q];
+    *reinterpret_cast<uint4*>(wfold + (size_t)c * KC + k) = pack8(v);
+    return;
+  }
+  __shared__ float red[3][16][64];
+  __shared__ float bred[3][64];
+  const int nt = C / 32;
+  const int ti = bid / nt, tj = bid - ti * nt;
+  const int c0 = ti * 32, d0 = tj * 32;
+  const int wv = t >> 6, lane = t & 63;
+  const int r = lane & 31, kh = (lane >> 5) * 8;
+  const bool with_bias = d0 == 0;
+  const int kq = K / 4, kbeg = wv * kq;  // this wave's K quarter (K % 256 == 0)
+  const uint16_t* pa = wt + (size_t)(c0 + r) * K + kbeg + kh;
+  const uint16_t* pb = wt + (size_t)(d0 + r) * K + kbeg + kh;
+  const float* ca_ = coef + kbeg + kh;
+  const float* cb_ = coef + K + kbeg + kh;
+  v16f acc = {};
+  float bacc = 0.f;
+  constexpr int B4 = 4;  // 16-k steps per batch
+  uint4 xa[B4], xb[B4], ya[B4], yb[B4];
+#pragma unroll
+  for (int q = 0; q < B4; ++q) {
+    xa[q] = *reinterpret_cast<const uint4*>(pa + q * 16);
+    xb[q] = *reinterpret_cast<const uint4*>(pb + q * 16);
+  }
+  for (int k0 = 0; k0 < kq; k0 += 16 * B4) {
+    const bool more = k0 + 16 * B4 < kq;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < B4; ++q) {
+        ya[q] = *reinterpret_cast<const uint4*>(pa + k0 + 16 * B4 + q * 16);
+        yb[q] = *reinterpret_cast<const uint4*>(pb + k0 + 16 * B4 + q * 16);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B4; ++q) {
+      const int kb = k0 + q * 16;
+      float a8[8];
+      load8(ca_ + kb, a8);
+      f8 fa = unpack8(xa[q]);
+      if (with_bias) {
+        float b8[8];
+        load8(cb_ + kb, b8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bacc = fmaf(fa.v[e], b8[e], bacc);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) fa.v[e] *= a8[e];
+      const uint4 qa = pack8(fa);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(fold_v8bf, qa),
+                                                    __builtin_bit_cast(fold_v8bf, xb[q]), acc, 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < B4; ++q) { xa[q] = ya[q]; xb[q] = yb[q]; }
+    }
+  }
+  if (wv > 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wv - 1][e][lane] = acc[e];
+    bred[wv - 1][lane] = bacc;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float v = acc[e] + red[0][e][lane] + red[1][e][lane] + red[2][e][lane];
+    const int row = 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
+    wfold[(size_t)(c0 + row) * KC + K + d0 + (lane & 31)] = f2bf(v);
+  }
+  if (with_bias) {
+    bacc += bred[0][lane] + bred[1][lane] + bred[2][lane];
+    bacc += __shfl_xor(bacc, 32, 64);  // the two k halves of row r
+    if (lane < 32) bias[c0 + r] = bacc;
+  }
+}
+
+// Weight gradient of the folded unit (ops/fused.py DgradFold path): with dy = k1*g + a*y + b and
+// y = W x, dW = sum_m dy^T x = diag(k1) T1 + diag(a) W Gram + b (x) colsum, where T1 = g^T x (the
+// ordinary weight gradient of g), Gram = x^T x and colsum = sum_m x.  out[k][c] (the flat gradient
+// buffer) += that; block 0 also adds dgamma += s1 * invstd, dbeta += s0 (the apply's job before).
+// Blocks: 32x32 tiles of out over (k, c); the K x C x C product W Gram runs through LDS.
+__global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(const float* __restrict__ t1,
+                                                            const float* __restrict__ gram,
+                                                            const float* __restrict__ colsum,
+                                                            const float* __restrict__ w, FoldCoef cf, int C,
+                                                            float* __restrict__ out, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta) {
+  const int K = cf.K, t = threadIdx.x;
+  const int nc = C / 32;
+  const int tk = blockIdx.x / nc, tc = blockIdx.x - tk * nc;
+  const int k0 = tk * 32, c0 = tc * 32;
+  if (blockIdx.x == 0 && dgamma != nullptr) {
+    for (int k = t; k < K; k += 256) {
+      const float is = cf.stats[K + k];
+      dgamma[k] += cf.sums[K + k] * is;
+      dbeta[k] += cf.sums[k];
+    }
+  }
+  __shared__ float sw[32][65], sg[64][33];
+  const int ty = t >> 4, tx = t & 15;  // outputs (k0 + 2ty + i, c0 + 2tx + j)
+  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  for (int q0 = 0; q0 < C; q0 += 64) {
+    for (int e = t; e < 32 * 64; e += 256) {
+      const int r = e >> 6, q = e & 63;
+      sw[r][q] = w[(size_t)(k0 + r) * C + q0 + q];
+    }
+    for (int e = t; e < 64 * 32; e += 256) {
+      const int q = e >> 5, cc = e & 31;
+      sg[q][cc] = gram[(size_t)(q0 + q) * C + c0 + cc];
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int q = 0; q < 64; ++q) {
+      const float w0 = sw[ty * 2][q], w1 = sw[ty * 2 + 1][q];
+      const float g0 = sg[q][tx * 2], g1 = sg[q][tx * 2 + 1];
+      acc[0][0] = fmaf(w0, g0, acc[0][0]); acc[0][1] = fmaf(w0, g1, acc[0][1]);
+      acc[1][0] = fmaf(w1, g0, acc[1][0]); acc[1][1] = fmaf(w1, g1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k = k0 + ty * 2 + i;
+    const float is = cf.stats[K + k], mu = cf.stats[k];
+    const float k1 = cf.gamma[k] * is;
+    const float k2 = cf.sums[K + k] * is * is * cf.invM;
+    const float a = -k1 * k2, b = -k1 * (cf.sums[k] * cf.invM - mu * k2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + tx * 2 + j;
+      const size_t o = (size_t)k * C + c;
+      out[o] += k1 * t1[o] + a * acc[i][j] + b * colsum[c];
+    }
+  }
+}
+
+void launch_bn_fold_wgrad(const float* t1, const float* gram, const float* colsum, const float* w,
+                          const float* stats, const float* gamma, const float* sums, int M, int C, int K,
+                          float* out, float* dgamma, float* dbeta, hipStream_t st) {
+  if (C % 64 != 0 || K % 32 != 0) throw std::runtime_error("bn_fold_wgrad: needs C % 64 == 0, K % 32 == 0");
+  FoldCoef cf{stats, gamma, sums, K, 1.f / (float)M};
+  hipLaunchKernelGGL(bn_fold_wgrad_kernel, dim3((K / 32) * (C / 32)), dim3(256), 0, st, t1, gram, colsum, w, cf, C,
+                     out, dgamma, dbeta);
+}
+
+void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
+                            int M, int C, int K, uint16_t* wfold, float* bias, hipStream_t st) {
+  if (C % 32 != 0 || K % 256 != 0 || K > kFoldMaxK)
+    throw std::runtime_error("bn_fold_weights: needs C % 32 == 0, K % 256 == 0, K <= 2048");
+  const int nG = (C / 32) * (C / 32);
+  const int nS = (int)(((int64_t)C * K / 8 + 255) / 256);
+  FoldCoef cf{stats, gamma, sums, K, 1.f / (float)M};
+  float* coef = bias + C;  // [2][K] scratch after the bias (the caller allocates C + 2K floats)
+  hipLaunchKernelGGL(bn_fold_coef_kernel, dim3(ceil_div(K, 256)), dim3(256), 0, st, cf, coef);
+  hipLaunchKernelGGL(bn_fold_weights_kernel, dim3(nG + nS), dim3(256), 0, st, wt, cf, coef, C, nG, wfold, bias);
+}
+
 __global__ void bn_eval_params_kernel(const float* rm, const float* rv, const float* gamma,
                                       const float* beta, float eps, int K, float* out) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -280,11 +510,6 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 }
 
 // ------------------------------------------------------------------- forward
-__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
-  float4 a = *reinterpret_cast<const float4*>(p);
-  float4 b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
 
 // RESBN: the residual is a raw (pre-BN) conv output with its own BatchNorm -- the projection
 // shortcut of a downsampling block.  It is normalised here and rounded to bf16 exactly as a

@@ -116,6 +116,12 @@ struct NtArgs {
   FastDiv div_ha;   // global image row -> image (divide by HA)
   // EPI_STATS: non-null -> per-channel fp64 totals of y and y^2 (kernels.h BnFwdFuse) instead of `part`
   double* sacc;
+  // K-concatenated second A operand (C64 loaders, one tap, dense 1x1 / stride 1 only): K-steps
+  // past CA read a2[m][CA2] -- B rows are then [CA weights | CA2 weights] (kernels.h DgradFold)
+  const uint16_t* a2;
+  uint32_t a2_bytes;
+  int CA2;
+  const float* bias;  // optional per-output-channel fp32 bias added to the accumulators (EPI_BNB)
 };
 
 // epilogue variants of the NT kernel
@@ -297,6 +303,22 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   const int wrow0 = m0 + wm * TM * 16;  // first GEMM row (pixel) of this wave
   const int wcol0 = n0 + wn * TN * 16;  // first output channel of this wave
 
+  if constexpr (EPI == EPI_BNB) {
+    if (P.bias != nullptr) {  // folded BN-backward constant term (DgradFold)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wcol0 + j * 16 + fq * 4;
+        const float4 bv = col < P.Nout ? *reinterpret_cast<const float4*>(P.bias + col)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if (wrow0 + i * 16 + fr < P.M) {  // rows past the GEMM stay 0 (the BN sums count them)
+            acc[i][j][0] += bv.x; acc[i][j][1] += bv.y; acc[i][j][2] += bv.z; acc[i][j][3] += bv.w;
+          }
+        }
+      }
+    }
+  }
   if constexpr (OP != OP_BF16) {
     // fp8: back to real units with the per-column factor (weight scale x activation scale)
     const float as = P.ascale != nullptr ? P.ascale[0] : 1.f;
@@ -660,6 +682,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(P.a2, P.a2_bytes);
 
   // A rows (pixels) and B rows (output channels) this lane fetches, fixed over the K loop
   // a_base: byte offset of (h0, w0, this lane's chunk) -- a tap adds the uniform scalar
@@ -683,6 +706,10 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
     }
     a_base[i] = (a_pix[i] + a_h0[i] * P.WA + a_w0[i]) * P.CA * EB + a_c[i] * 16;
   }
+  // second A operand: GEMM row m == pixel m (dense 1x1); rows >= M lie past a2_bytes and read 0
+  int a2_base[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) a2_base[i] = (m0 + (wid * A_PW + i) * RPI + lr) * P.CA2 * EB + a_c[i] * 16;
   int b_row[B_PW], b_c[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
@@ -692,7 +719,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
     b_row[i] = n < P.Nout ? n * P.Kg : -1;
   }
 
-  const int nk = C64 ? P.ntaps * (P.CA / KE) : (P.Kg + KE - 1) / KE;
+  const int nk = C64 ? P.ntaps * (P.CA / KE) + (P.a2 != nullptr ? P.CA2 / KE : 0) : (P.Kg + KE - 1) / KE;
 
   // C64 path: per A row, bit t of a_inv = tap t (= ti*tns + tj) reads outside the image.  Built
   // once from the separable row / column validity; a K-step then turns it into a 0 / all-ones
@@ -752,7 +779,10 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
     char* Bs = As + BM * CFG::ROWB;
     if constexpr (C64) {
       const int tap = k_ti * P.tns + k_tj;
-      if (q < A_PW) {
+      if (q < A_PW && k_chb >= P.CA) {  // K-concatenated second operand (P.a2)
+        const int i = q;
+        glds16(ra2, As + (wid * A_PW + i) * 1024, valid ? (uint32_t)(a2_base[i] + (k_chb - P.CA) * EB) : OOB);
+      } else if (q < A_PW) {
         const int i = q;
         const int dr = P.dr0 + k_ti * P.dstep, ds = P.ds0 + k_tj * P.dstep;
         const int tdelta = ((dr * P.WA + ds) * P.CA + k_chb) * EB;
@@ -806,7 +836,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (nt_min_waves<WM * WN, HALO>()))
   auto advance = [&]() {
     if constexpr (C64) {
       k_chb += KE;
-      if (k_chb == P.CA) {
+      if (k_chb == P.CA && P.a2 == nullptr) {  // with a2 (one tap) the channel index runs on past CA
         k_chb = 0;
         if (++k_tj == P.tns) { k_tj = 0; ++k_ti; }
       }
@@ -1065,11 +1095,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   const int lr = lane >> 3, lj = lane & 7;  // row within a DMA instruction (8 rows), LDS chunk slot
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(P.a, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(P.b, P.b_bytes);
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(P.a2, P.a2_bytes);
 
   // this lane's DMA rows: piece i (0, 1) of half h covers half-local rows r = (wid*2 + i)*8 + lr;
   // half-local row r of X half h is GEMM row (r / HX)*2*HX + h*HX + r % HX (wave-row blocks), of W
   // half h channel (r / HW)*2*HW + h*HW + r % HW
-  int a_base[2][2], b_row[2][2], b_c[2][2];
+  int a_base[2][2], a2_base[2][2], b_row[2][2], b_c[2][2];
   uint32_t a_inv[2][2];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -1090,6 +1121,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
         w0 = (int)jj * P.asw + P.aoff_w;
       }
       a_base[h][i] = (pix + h0 * P.WA + w0) * P.CA * EB + sc * 16;
+      a2_base[h][i] = m * P.CA2 * EB + sc * 16;  // dense 1x1: row m == pixel m; m >= M reads 0
       // tap validity bitmask (see igemm_nt_kernel): bit t set = tap t reads outside the image
       const int nr = P.tnr, ns = P.tns;
       const int hb = h0 + P.dr0, wb = w0 + P.ds0;
@@ -1107,12 +1139,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
     }
 
   // K-step state of the NEXT step to issue (ti, tj, channel block), advanced once per step
-  const int nk = P.ntaps * (P.CA / KE);
+  const int nk = P.ntaps * (P.CA / KE) + (P.a2 != nullptr ? P.CA2 / KE : 0);
   int q_ti = 0, q_tj = 0, q_chb = 0, q_kt = 0;
   auto advance = [&]() {
     ++q_kt;
     q_chb += KE;
-    if (q_chb == P.CA) {
+    if (q_chb == P.CA && P.a2 == nullptr) {  // with a2 (one tap) the channel index runs on past CA
       q_chb = 0;
       if (++q_tj == P.tns) { q_tj = 0; ++q_ti; }
     }
@@ -1121,7 +1153,11 @@ __global__ void __launch_bounds__(WM * WN * 64, (NtqCfg<WM, WN, TMQ, TNQ>::MIN_W
   auto issue = [&](int op, int h, int st) {
     const bool valid = q_kt < nk;
     char* dst = smem + st * STAGE + (op == 0 ? h * QX : 2 * QX + h * QW) + wid * 2048;
-    if (op == 0) {
+    if (op == 0 && q_chb >= P.CA) {  // K-concatenated second operand (P.a2)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        glds16(ra2, dst + i * 1024, valid ? (uint32_t)(a2_base[h][i] + (q_chb - P.CA) * EB) : OOB);
+    } else if (op == 0) {
       const int tap = q_ti * P.tns + q_tj;
       const int dr = P.dr0 + q_ti * P.dstep, ds = P.ds0 + q_tj * P.dstep;
       const int tdelta = ((dr * P.WA + ds) * P.CA + q_chb) * EB;
@@ -1257,6 +1293,8 @@ struct TnF8Args {
   int HoWo, Wo, Ho;
   int steps_per_split, nsteps;
   int adv_r, adv_qh, adv_qn;  // 128 reduction rows = (adv_qn images, adv_qh output rows, adv_r columns)
+  float* zero;                // optional: zero_n floats workgroup 0 clears (a consumed BN-sum
+  int zero_n;                 //   accumulator; as wgrad.hip, no memset launch)
 };
 
 template <int ROWB>
@@ -1294,6 +1332,8 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
   constexpr int TM = BMG / 32, TN = 4;         // 2 x 2 waves of (BMG/2) x 64
   static_assert(A_PW * 1024 * WAVES == A_BYTES && B_PW * 1024 * WAVES == B_BYTES, "tile DMA split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (P.zero != nullptr && blockIdx.x == 0)  // ordered after the accumulator's consumer by the caller
+    for (int i = threadIdx.x; i < P.zero_n; i += blockDim.x) P.zero[i] = 0.f;
 
   const int ntn = (P.Ncols + 127) / 128;
   const int ntm = (P.Kout + BMG - 1) / BMG;
@@ -1537,8 +1577,8 @@ static bool setup_halo(NtArgs& a, int R, int S, int tap_stride, int pad) {
 // M >= 786432 on forward (stats epilogue) GEMMs and 64-column dgrads.
 // Test hook (conv_nt_force): pin the K32 / K64 main loop of every NT launch, or disable the
 // 128x256 short-K tile, so tests can compare the policy's alternatives bit for bit.  -1: policy.
-static int g_force_k32 = -1, g_force_mid = -1;
-void conv_nt_force(int k32, int mid) { g_force_k32 = k32; g_force_mid = mid; }
+static int g_force_k32 = -1, g_force_mid = -1, g_force_wide = -1;
+void conv_nt_force(int k32, int mid, int wide) { g_force_k32 = k32; g_force_mid = mid; g_force_wide = wide; }
 
 static bool nt_k32(const NtArgs& a, int epi) {
   if (g_force_k32 >= 0) return g_force_k32 == 1;
@@ -1551,7 +1591,7 @@ static bool nt_k32(const NtArgs& a, int epi) {
 // pays with enough blocks (>= 196, measured on the ResNet-50 shape classes: +10-20% on the 28x28
 // and 14x14 layers, -40% on 7x7 with 98 blocks) and a K loop longer than one step.
 static bool use_wide_tile(int M, int Nout, int kg_bytes) {
-  if (Nout < 256) return false;
+  if (Nout < 256 || g_force_wide == 0) return false;
   const int64_t blocks = (int64_t)((M + 255) / 256) * ((Nout + 255) / 256);
   return kg_bytes >= 256 && blocks >= 196;
 }
@@ -1738,8 +1778,11 @@ int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes) {
 template <int OP>
 static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale, const float* ascale,
                             uint16_t* dx, const uint16_t* addend, const ConvShape& s, hipStream_t st,
-                            const BnBwdFuse* bn, int addend_sub) {
+                            const BnBwdFuse* bn, int addend_sub, const DgradFold* fold = nullptr) {
   if (addend_sub != 0 && addend_sub != 2) throw std::runtime_error("conv_dgrad: addend_sub must be 0 or 2");
+  if (fold != nullptr && (OP != OP_BF16 || s.R != 1 || s.S != 1 || s.stride != 1 || s.pad != 0 ||
+                          fold->CA2 != s.C || s.C % 64 != 0 || s.K % 64 != 0))
+    throw std::runtime_error("conv_dgrad: the folded BN backward needs a bf16 1x1 / stride-1 conv, 64-channel multiples");
   constexpr int EB = OP == OP_BF16 ? 2 : 1;
   const int str = s.stride;
   // full: dy rows are whole 128-byte K-steps per tap (the C64 loader, any stride).  fp8 with
@@ -1782,6 +1825,12 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       if (a.ntaps > 32) throw std::runtime_error("conv_dgrad: more than 32 taps per parity class");
       a.tr0 = r0; a.ts0 = s0; a.tstep = str;
       a.dr0 = (ph + s.pad - r0) / str; a.ds0 = (pw + s.pad - s0) / str; a.dstep = -1;
+      if (fold != nullptr) {  // K-concatenated [dy | z] against B rows [C][K + C] (DgradFold)
+        a.a2 = fold->a2; a.CA2 = fold->CA2; a.bias = fold->bias;
+        a.a2_bytes = (uint32_t)((int64_t)a.M * fold->CA2 * EB);
+        a.Kg += fold->CA2;
+        a.b_bytes = (uint32_t)((int64_t)s.C * a.Kg * EB);
+      }
       if (bn != nullptr) {
         a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part; a.bn_acc = bn->acc;
         a.bn_mask = bn->mask; a.bn_group0 = group0;
@@ -1800,8 +1849,9 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
 }
 
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
-                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn, int addend_sub) {
-  conv_dgrad_impl<OP_BF16>(dy, wt, nullptr, nullptr, dx, addend, s, st, bn, addend_sub);
+                       const ConvShape& s, hipStream_t st, const BnBwdFuse* bn, int addend_sub,
+                       const DgradFold* fold) {
+  conv_dgrad_impl<OP_BF16>(dy, wt, nullptr, nullptr, dx, addend, s, st, bn, addend_sub, fold);
 }
 
 void launch_conv_dgrad_fp8(const uint8_t* dy, const uint8_t* wt, const float* oscale, const float* ascale,
@@ -1828,7 +1878,8 @@ void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]) {
 }
 
 void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
-                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st) {
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st, float* zero,
+                           int zero_n) {
   if (s.C % 16 != 0 || s.K % 64 != 0) throw std::runtime_error("conv_wgrad_fp8: needs C % 16 == 0, K % 64 == 0");
   int pl[4];
   conv_wgrad_fp8_plan(s, pl);
@@ -1846,6 +1897,7 @@ void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* d
   a.adv_r = 128 % s.Wo;
   a.adv_qh = (128 / s.Wo) % s.Ho;
   a.adv_qn = (128 / s.Wo) / s.Ho;
+  a.zero = zero; a.zero_n = zero_n;
   if (!accumulate) hipMemsetAsync(dw, 0, (size_t)s.K * a.Ncols * sizeof(float), st);
   const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 && s.H == s.Ho && s.W == s.Wo;
   const int grid = pl[1] * pl[2];

@@ -68,7 +68,7 @@ int conv_nt_group_rows(int M, int Nout, int kg_bytes);
 // (BM, BN) of the NT workgroup tile the fwd / dgrad launch of such a GEMM runs (test introspection)
 void conv_nt_tile(int M, int Nout, int kg_bytes, int* bm, int* bn);
 // tests: force the NT main loop (k32 1 / 0) and disable the 128x256 tile (mid 0); -1 = policy
-void conv_nt_force(int k32, int mid);
+void conv_nt_force(int k32, int mid, int wide = -1);
 // number of stream-K NT launches so far in this process (tests: which path ran)
 // PDT_NT_TIMING builds (scripts/build_variant.sh): per-workgroup phase timestamps of NT launches
 // (s_memtime at start / first operands in LDS / main loop done / epilogue stats done / end, plus
@@ -110,9 +110,30 @@ struct BnBwdFuse {
 int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes = 2);
 // addend_sub = 2: addend is a compact [N, ceil(H/2), ceil(W/2), C] map added at even (h, w) only
 // (the input gradient of a 1x1/s2 projection shortcut, computed as a dense 1x1 dgrad)
+// BN backward folded into a 1x1 / stride-1 input gradient (ops/fused.py, last unit of a
+// bottleneck): with dy = k1*g + a*y + b per output channel k (the BN-backward apply written out) and
+// y = W z (the conv's own output), dx = W^T diag(k1) g + (W^T diag(a) W) z + W^T b -- one GEMM over
+// the K-concatenation [g | z] with B rows [wt*k1 | G] (bn_fold_weights) plus a per-channel bias, so
+// the apply that materialises dy leaves the critical path (it still feeds the weight gradient).
+struct DgradFold {
+  const uint16_t* a2;  // z: [M][CA2] bf16, the conv input (CA2 = its channels = the dgrad's Nout)
+  int CA2;
+  const float* bias;   // [Nout] fp32
+};
+// wfold[C][K + C] bf16 and bias[C] fp32 (followed by 2K floats of scratch) of a DgradFold for the
+// 1x1 conv with transposed bf16
+// weights wt[C][K], BN statistics stats[4][K] (mean, invstd, ...), gamma[K] and backward sums
+// sums[2][K] (sum g, sum g*(y - mean)) over M rows
+void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
+                            int M, int C, int K, uint16_t* wfold, float* bias, hipStream_t st);
+// its weight gradient: out[K][C] += diag(k1) t1 + diag(a) w gram + b colsum^T (t1 = g^T x [K][C],
+// gram = x^T x [C][C], colsum = sum of x [C], w [K][C] fp32); dgamma/dbeta (optional) += s1 * invstd, s0
+void launch_bn_fold_wgrad(const float* t1, const float* gram, const float* colsum, const float* w,
+                          const float* stats, const float* gamma, const float* sums, int M, int C, int K,
+                          float* out, float* dgamma, float* dbeta, hipStream_t st);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
                        const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr,
-                       int addend_sub = 0);
+                       int addend_sub = 0, const DgradFold* fold = nullptr);
 // dw[K][R][S][C] (fp32) = wgrad(dy, x).  Split-K partials are combined with fp32 atomics, or
 // (deterministic) in private slabs ws[conv_wgrad_ws_floats()] reduced in fixed order.
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
@@ -124,7 +145,8 @@ void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]);
 // fp32 atomics (non-deterministic order); C % 16 == 0, K % 64 == 0.  plan: (bmg, tiles, splits, steps/split)
 void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]);
 void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
-                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st,
+                           float* zero = nullptr, int zero_n = 0);
 // zero / zero_n: optional fp32 buffer the weight-gradient kernel clears (workgroup 0) -- the BN-sum
 // accumulator whose consumer is ordered before this launch (ops/fused.py PDT_BN_ACC)
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,

@@ -1135,10 +1135,38 @@ class _ResidualBlock(torch.autograd.Function):
                                      st)
             else:
                 g, sums = pre  # g = dz * relu'(unit i), reduced in the producing epilogue
-                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None, st)
                 dres = g
+            fold = None
+            if pre is not None and _fold_ok(i, last, w, xin, st, pd, tr, det, side, ctx.fp8b, params):
+                # BN backward folded into the input gradient (kernels.h DgradFold): the dgrad below
+                # reads [g | x] against [w*k1 | W^T diag(a) W] + bias instead of the applied dy, so the
+                # apply -- now feeding only the weight gradient -- runs on the side stream with it
+                wt = _packed_crsk(w)
+                if wt is None:
+                    wt = C.pack_weight_t(w)
+                global FOLD_CALLS
+                FOLD_CALLS += 1
+                k_, c_ = w.shape[0], w.shape[1]
+                count = y.numel() // k_
+                fold = C.bn_fold_weights(wt.view(c_, k_), stt, gamma, sums, count)
+                # the weight gradient without dy either: dW = diag(k1) g^T x + diag(a) W x^T x + b sum(x),
+                # on the side stream (also the BN parameter gradients and the accumulator re-zero)
+                streams.fork(side, g, stt, sums, xin)
+                with torch.cuda.stream(side):
+                    t1 = C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, False)
+                    gram = C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, False)
+                    colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
+                    dfr = deferred.pop(5 * i, None)
+                    C.bn_fold_wgrad(t1, gram, colsum, w, stt, gamma, sums, count, _grad_sink(params[5 * i]),
+                                    dfr[1] if dfr is not None else None, dfr[2] if dfr is not None else None)
+                    if dfr is not None:
+                        dfr[0].zero_()
+                sunk.append(params[5 * i])
+            elif pre is not None:
+                dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None, st)
             pre = None
-            wgrad(5 * i, dy, xin, st, pd, d8, in8[i] if in8 else None)
+            if fold is None:
+                wgrad(5 * i, dy, xin, st, pd, d8, in8[i] if in8 else None)
             if last:
                 g_short = dres
                 if ds_cfg is not None and nch > 1 and ds_br is not None:
@@ -1150,7 +1178,13 @@ class _ResidualBlock(torch.autograd.Function):
                     ds_join = (main, streams.join(ds_br, main, addend_br), addend_br)
             if i > 0:
                 yp, sttp = units[i - 1][1], units[i - 1][2]
-                if _FUSE_DGRAD_BN:
+                if fold is not None:
+                    j = 5 * (i - 1)
+                    acc = _bacc(params[j + 1], sttp.shape[1])
+                    pre = C.conv_dgrad_bn_fold(g, xin, fold[0], fold[1], yp, None, sttp, 2, acc)
+                    deferred[j] = (acc, _grad_sink(params[j + 1]), _grad_sink(params[j + 2]))
+                    sunk.extend([params[j + 1], params[j + 2]])
+                elif _FUSE_DGRAD_BN:
                     pre = dgrad_bn(5 * (i - 1), dy, d8, w, xin_shape, st, pd, None, yp, None, sttp, 2)
                 else:
                     dz = dgrad(dy, d8, w, xin_shape, st, pd, None)
@@ -1189,6 +1223,41 @@ class _ResidualBlock(torch.autograd.Function):
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
         return (dz, None, None, None, *grads)
+
+
+# Fold the last unit's BN backward into its 1x1 input gradient (DgradFold) -- ResNet-50 b256 in the
+# same calls: 18.15 vs 18.29 and 18.27 vs 18.54 ms/step (r6r / r6s); removing that apply altogether
+# bounds the gain at 1.47 ms (r6f), the rest is spent in the fold-weight kernels on the critical
+# stream (~20 us per block in-step) and the larger dgrad K.
+_FOLD_BN = True
+FOLD_CALLS = 0  # folded units so far (tests check that the path engaged)
+
+
+def _fold_ok(i, last, w, xin, st, pd, tr, det, side, fp8b, params) -> bool:
+    """May the last unit of a bottleneck fold its BN backward into its 1x1 input gradient
+    (kernels.h DgradFold)?  bf16, non-deterministic (acc-mode sums), training, a weight-gradient
+    side stream, a 1x1 / stride-1 conv over a materialised input, and gradient sinks for the BN of
+    the unit before (its sums go to an atomic accumulator)."""
+    if not (_FOLD_BN and last and i > 0 and tr and not det and side is not None and not fp8b and _BN_ACC
+            and _FUSE_DGRAD_BN and xin is not None):
+        return False
+    k, c, r, s_ = w.shape
+    if r != 1 or s_ != 1 or st != 1 or pd != 0 or k % 256 or k > 2048 or c % 64 or xin.shape[3] != c:
+        return False
+    j = 5 * (i - 1)
+    return (_grad_sink(params[j + 1]) is not None and _grad_sink(params[j + 2]) is not None
+            and _grad_sink(params[5 * i]) is not None)
+
+
+_ZSTATS = {}
+
+
+def _zero_stats(c, dev):
+    """Zero [4, c] BN statistics (a column sum through bn_act_bwd_reduce), cached per device."""
+    z = _ZSTATS.get((c, dev))
+    if z is None:
+        z = _ZSTATS[(c, dev)] = torch.zeros(4, c, device=dev)
+    return z
 
 
 def _grad_sink(p):

@@ -70,8 +70,12 @@ def main():
     ap.add_argument("--bn", action="store_true", help="also time dgrad with the fused BN-backward epilogue")
     ap.add_argument("--det", action="store_true", help="wgrad in deterministic mode (split-K slabs + reduce)")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="which products to time (others report 0)")
+    ap.add_argument("--force", default=None,
+                    help="NT tile-policy test hook 'k32/mid/wide' (-1 policy, 0 off, 1 on): C.conv_nt_force")
     a = ap.parse_args()
     C = native()
+    if a.force:
+        C.conv_nt_force(*[int(v) for v in a.force.split("/")])
     dev = torch.device("cuda:0")
     N = a.batch
     rows = []

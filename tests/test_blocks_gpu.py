@@ -98,6 +98,7 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc
 
     ddp.space.grad_flat.zero_()
     ddp.space.attach_grads()
+    folds0 = fused.FOLD_CALLS
     out_n = blocks_n[1].forward_native(blocks_n[0].forward_native(x_n))
     out_r = blocks_r[1](blocks_r[0](x_r))
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -107,6 +108,9 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc
     out_r.backward(dz32)
     out_a.backward(dz32)
     torch.cuda.synchronize()
+    # the folded BN backward (ops.fused DgradFold) runs in block 0's last unit of a Bottleneck pair
+    # whenever the atomic BN sums are on
+    assert (fused.FOLD_CALLS > folds0) == (bn_acc and arch == "resnet50"), (fused.FOLD_CALLS, folds0)
 
     errs, yard = {}, {}
     errs["out"] = _rel(out_n.permute(0, 3, 1, 2), out_r)

@@ -960,3 +960,56 @@ def test_stem_pool_argmax_y_reduction(gpu, native_ext, n, h, w):
     got = C.bn_act_bwd_reduce(dpool, u, u, stats, 2)
     torch.cuda.synchronize()
     assert _rel_err(got, ref) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 256), (2, 7, 9, 128, 512), (3, 28, 28, 64, 256),
+                                   (2, 7, 7, 512, 2048), (9, 32, 32, 128, 512), (16, 56, 56, 256, 1024)])
+def test_folded_bn_backward_dgrad_matches_apply_then_dgrad(gpu, native_ext, shape):
+    """DgradFold (ops/fused.py, last unit of a bottleneck): dx = [g | z] x [wt*k1 | G]^T + bias with
+    G = W^T diag(a) W equals the BN-backward apply (dy = k1 g + a y + b) followed by the 1x1 dgrad,
+    against an fp32 reference of that composition; the fused epilogue's BN sums (acc mode) too."""
+    C = native_ext
+    n, h, w_, c, k = shape
+    g_ = torch.Generator().manual_seed(21)
+    z_in = torch.relu(torch.randn(n, h, w_, c, generator=g_)).to(torch.bfloat16).to(gpu)
+    w = (torch.randn(k, c, 1, 1, generator=g_) / c ** 0.5).to(gpu).contiguous(memory_format=torch.channels_last)
+    y, part = C.conv_fwd(z_in, C.pack_weight(w, c), 1, 0, True)
+    M = n * h * w_
+    gamma = (1 + 0.2 * torch.randn(k, generator=g_)).to(gpu)
+    beta = (0.1 * torch.randn(k, generator=g_)).to(gpu)
+    stats = C.bn_finalize(part, M, torch.zeros(k, device=gpu), torch.ones(k, device=gpu), gamma, beta, 0.1, 1e-5)
+    g = (torch.randn(n, h, w_, k, generator=g_) * (torch.rand(n, h, w_, k, generator=g_) > 0.4)).to(torch.bfloat16).to(gpu)
+    sums = C.bn_act_bwd_reduce(g, g, y, stats, 0)
+    # the unit before (whose BN the dgrad epilogue reduces): y_prev, its stats, mask 2
+    y_prev = torch.randn(n, h, w_, c, generator=g_).to(torch.bfloat16).to(gpu)
+    st_prev = torch.stack([torch.zeros(c), torch.ones(c), torch.ones(c) * 0.7, torch.ones(c) * 0.05]).to(gpu).contiguous()
+    # reference composition on the native kernels: apply, then BN-fused dgrad
+    dy, _ = C.bn_act_bwd_apply(g, g, y, stats, gamma, sums, 0, True, False)
+    acc_a = torch.zeros(2, c, device=gpu)
+    dx_a, _ = C.conv_dgrad_bn(dy, w, [n, h, w_, c], 1, 0, None, y_prev, None, st_prev, 2, acc=acc_a)
+    # folded
+    wt = C.pack_weight_t(w).view(c, k)
+    wfold, bias = C.bn_fold_weights(wt, stats, gamma, sums, M)
+    acc_b = torch.zeros(2, c, device=gpu)
+    dx_b, s_b = C.conv_dgrad_bn_fold(g, z_in, wfold, bias, y_prev, None, st_prev, 2, acc_b)
+    assert s_b.data_ptr() == acc_b.data_ptr()
+    # fp32 reference: BN backward apply in fp32 from the same bf16 g and y, dgrad in fp32, mask 2
+    mu, inv = stats[0], stats[1]
+    gf, yf = g.float().reshape(-1, k), y.float().reshape(-1, k)
+    s0, s1 = gf.sum(0), (gf * (yf - mu)).sum(0)
+    k1 = gamma * inv
+    dyf = k1 * (gf - s0 / M - (yf - mu) * (s1 * inv * inv / M))
+    dxf = (dyf @ w.reshape(k, c).float()).reshape(n, h, w_, c)
+    on = (y_prev.float() * st_prev[2] + st_prev[3]) > 0
+    dxf = torch.where(on, dxf, 0.0)
+    rel = lambda a_, b_: ((a_.float() - b_).norm() / b_.norm()).item()  # noqa: E731
+    assert rel(dx_a, dxf) < 1e-2
+    assert rel(dx_b, dxf) < 1e-2, (rel(dx_b, dxf), rel(dx_a, dxf))
+    assert rel(dx_b, dx_a.float()) < 1e-2
+    # the epilogue's BN sums (sum g, sum g*y at mean 0): within 1 % of the summed magnitudes (the sums
+    # themselves cancel), and as close to the unfolded path's
+    d2, yp = dxf.reshape(-1, c), y_prev.float().reshape(-1, c)
+    ref_sums = torch.stack([d2.sum(0), (d2 * yp).sum(0)])
+    mag = torch.stack([d2.abs().sum(0), (d2 * yp).abs().sum(0)])
+    assert ((acc_b - ref_sums).abs() <= 1e-2 * mag + 1e-6).all(), ((acc_b - ref_sums).abs() / mag).max()
+    assert ((acc_a - ref_sums).abs() <= 1e-2 * mag + 1e-6).all(), ((acc_a - ref_sums).abs() / mag).max()
