@@ -552,14 +552,6 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
     st = sst.stream();
   }
   Tensor r;
-  // a consumed BN-sum accumulator: the kernel's workgroup 0 clears it (as conv_wgrad_side)
-  float* zp = nullptr;
-  int zn = 0;
-  if (zero.has_value() && zero->defined()) {
-    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous(), "zero: contiguous fp32");
-    zp = zero->data_ptr<float>();
-    zn = (int)zero->numel();
-  }
   if (out.has_value() && out->defined()) {
     const Tensor& o = *out;
     TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 4 && o.size(0) == K && o.size(1) == C &&
@@ -568,14 +560,19 @@ Tensor conv_wgrad_fp8(int64_t side, const Tensor& dy8, const Tensor& x8, const T
     for (int d = 0; d < 4; ++d)
       TORCH_CHECK(o.size(d) == 1 || o.stride(d) == want[d], "wgrad out must be channels_last (KRSC) dense");
     pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
-                               x_deq.data_ptr<float>(), o.data_ptr<float>(), s, true, st, zp, zn);
+                               x_deq.data_ptr<float>(), o.data_ptr<float>(), s, true, st);
     r = o;
   } else {
     auto dwp = at::empty({K, R, S, C}, x8.options().dtype(at::kFloat));
     pdt::launch_conv_wgrad_fp8(dy8.data_ptr<uint8_t>(), x8.data_ptr<uint8_t>(), dy_deq.data_ptr<float>(),
-                               x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st, zp, zn);
+                               x_deq.data_ptr<float>(), dwp.data_ptr<float>(), s, false, st);
     r = dwp.permute({0, 3, 1, 2});
   }
+  // a consumed BN-sum accumulator: cleared by a memset AFTER the kernel (the bf16 weight gradient
+  // clears it in its workgroup 0 instead; done that way here, the fp8 ResNet-50 parity runs fell
+  // behind in 4 of 7 runs against 0 of 7 with the memset -- profiles/r6_fp8_parity.txt)
+  if (zero.has_value() && zero->defined())
+    TORCH_CHECK(hipMemsetAsync(zero->data_ptr(), 0, zero->nbytes(), st) == hipSuccess, "memset");
   if (side != 0) {
     auto sst = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(side), dev);
     for (const Tensor* t : {&dy8, &x8, &dy_deq, &x_deq})
@@ -1239,15 +1236,17 @@ Tensor top1_correct(const Tensor& logits_in, const Tensor& labels) {
 }
 
 // --------------------------------------------------------------------- sgd
-void sgd_step(Tensor p, const Tensor& g, Tensor buf, double lr, double momentum, double dampening,
-              double wd, bool nesterov, bool first, double grad_scale,
+void sgd_step(Tensor p, const Tensor& g, const std::optional<Tensor>& buf_opt, double lr, double momentum,
+              double dampening, double wd, bool nesterov, bool first, double grad_scale,
               const std::optional<Tensor>& p_bf16) {
   check_cuda(p, "param");
   check_cuda(g, "grad");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 flat buffers only");
   TORCH_CHECK(p.numel() == g.numel(), "param/grad size mismatch");
   bool mom = momentum != 0.0;
+  Tensor buf = buf_opt.has_value() ? *buf_opt : Tensor();  // momentum 0: no buffer (None)
   if (mom) {
+    TORCH_CHECK(buf.defined(), "sgd_step: momentum != 0 needs a momentum buffer");
     check_cuda(buf, "momentum_buffer");
     TORCH_CHECK(buf.numel() == p.numel(), "momentum buffer size mismatch");
   }

@@ -1293,8 +1293,6 @@ struct TnF8Args {
   int HoWo, Wo, Ho;
   int steps_per_split, nsteps;
   int adv_r, adv_qh, adv_qn;  // 128 reduction rows = (adv_qn images, adv_qh output rows, adv_r columns)
-  float* zero;                // optional: zero_n floats workgroup 0 clears (a consumed BN-sum
-  int zero_n;                 //   accumulator; as wgrad.hip, no memset launch)
 };
 
 template <int ROWB>
@@ -1332,8 +1330,6 @@ __global__ void __launch_bounds__(256, 2) igemm_tn_f8_kernel(const TnF8Args P) {
   constexpr int TM = BMG / 32, TN = 4;         // 2 x 2 waves of (BMG/2) x 64
   static_assert(A_PW * 1024 * WAVES == A_BYTES && B_PW * 1024 * WAVES == B_BYTES, "tile DMA split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (P.zero != nullptr && blockIdx.x == 0)  // ordered after the accumulator's consumer by the caller
-    for (int i = threadIdx.x; i < P.zero_n; i += blockDim.x) P.zero[i] = 0.f;
 
   const int ntn = (P.Ncols + 127) / 128;
   const int ntm = (P.Kout + BMG - 1) / BMG;
@@ -1878,8 +1874,7 @@ void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]) {
 }
 
 void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
-                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st, float* zero,
-                           int zero_n) {
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st) {
   if (s.C % 16 != 0 || s.K % 64 != 0) throw std::runtime_error("conv_wgrad_fp8: needs C % 16 == 0, K % 64 == 0");
   int pl[4];
   conv_wgrad_fp8_plan(s, pl);
@@ -1897,7 +1892,6 @@ void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* d
   a.adv_r = 128 % s.Wo;
   a.adv_qh = (128 / s.Wo) % s.Ho;
   a.adv_qn = (128 / s.Wo) / s.Ho;
-  a.zero = zero; a.zero_n = zero_n;
   if (!accumulate) hipMemsetAsync(dw, 0, (size_t)s.K * a.Ncols * sizeof(float), st);
   const bool pw = s.R == 1 && s.S == 1 && s.stride == 1 && s.sw() == 1 && s.pad == 0 && s.H == s.Ho && s.W == s.Wo;
   const int grid = pl[1] * pl[2];

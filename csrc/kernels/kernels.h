@@ -145,8 +145,7 @@ void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]);
 // fp32 atomics (non-deterministic order); C % 16 == 0, K % 64 == 0.  plan: (bmg, tiles, splits, steps/split)
 void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]);
 void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
-                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st,
-                           float* zero = nullptr, int zero_n = 0);
+                           float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
 // zero / zero_n: optional fp32 buffer the weight-gradient kernel clears (workgroup 0) -- the BN-sum
 // accumulator whose consumer is ordered before this launch (ops/fused.py PDT_BN_ACC)
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,

@@ -294,6 +294,17 @@ def test_sgd_flat(gpu, native_ext, nesterov):
     assert torch.allclose(buf, b2, atol=1e-6)
 
 
+def test_sgd_flat_without_momentum(gpu, native_ext):
+    """momentum 0 (torch.optim.SGD's default): no momentum buffer at all -- p -= lr * (g + wd * p)"""
+    C = native_ext
+    n = 10001
+    p = torch.randn(n, device=gpu)
+    gr = torch.randn(n, device=gpu)
+    want = p - 0.1 * (gr + 1e-4 * p)
+    C.sgd_step(p, gr, None, 0.1, 0.0, 0.0, 1e-4, False, True, 1.0)
+    assert torch.allclose(p, want, atol=1e-6)
+
+
 def test_rccl_comm_single_rank(gpu, native_ext):
     C = native_ext
     comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1, 0)
