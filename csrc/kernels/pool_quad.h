@@ -13,6 +13,24 @@ namespace pdt {
 // outputs coincide one to one (Ho = ceil(H/2) for k3/s2/p1).
 struct PoolQuad { f8 g[4]; };  // g[dh*2 + dw]
 
+// combine step of the gather on already-loaded (argmax, gradient) pairs of the four windows
+__device__ __forceinline__ PoolQuad pool_grad_quad_regs(const uint2 (&id)[4], const f8 (&gw)[4]) {
+  PoolQuad q;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t s[4];
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) s[wi] = ((j < 4 ? id[wi].x : id[wi].y) >> (8 * (j & 3))) & 0xffu;
+    const float g00 = gw[0].v[j], g01 = gw[1].v[j], g10 = gw[2].v[j], g11 = gw[3].v[j];
+    q.g[0].v[j] = s[0] == 4u ? g00 : 0.f;
+    q.g[1].v[j] = (s[0] == 5u ? g00 : 0.f) + (s[1] == 3u ? g01 : 0.f);
+    q.g[2].v[j] = (s[0] == 7u ? g00 : 0.f) + (s[2] == 1u ? g10 : 0.f);
+    q.g[3].v[j] = ((s[0] == 8u ? g00 : 0.f) + (s[1] == 6u ? g01 : 0.f)) +
+                  ((s[2] == 2u ? g10 : 0.f) + (s[3] == 0u ? g11 : 0.f));
+  }
+  return q;
+}
+
 __device__ __forceinline__ PoolQuad pool_grad_quad(const uint4* __restrict__ dp, const uint2* __restrict__ idx,
                                                    int n, int a, int b, int c8, int C8, int Ho, int Wo) {
   uint2 id[4];
@@ -30,20 +48,7 @@ __device__ __forceinline__ PoolQuad pool_grad_quad(const uint4* __restrict__ dp,
       for (int j = 0; j < 8; ++j) gw[wi].v[j] = 0.f;
     }
   }
-  PoolQuad q;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint32_t s[4];
-#pragma unroll
-    for (int wi = 0; wi < 4; ++wi) s[wi] = ((j < 4 ? id[wi].x : id[wi].y) >> (8 * (j & 3))) & 0xffu;
-    const float g00 = gw[0].v[j], g01 = gw[1].v[j], g10 = gw[2].v[j], g11 = gw[3].v[j];
-    q.g[0].v[j] = s[0] == 4u ? g00 : 0.f;
-    q.g[1].v[j] = (s[0] == 5u ? g00 : 0.f) + (s[1] == 3u ? g01 : 0.f);
-    q.g[2].v[j] = (s[0] == 7u ? g00 : 0.f) + (s[2] == 1u ? g10 : 0.f);
-    q.g[3].v[j] = ((s[0] == 8u ? g00 : 0.f) + (s[1] == 6u ? g01 : 0.f)) +
-                  ((s[2] == 2u ? g10 : 0.f) + (s[3] == 0u ? g11 : 0.f));
-  }
-  return q;
+  return pool_grad_quad_regs(id, gw);
 }
 
 // (n, a, b) of quad / pooled-output index qd (32-bit math; the host bounds the sizes)

@@ -291,6 +291,10 @@ void launch_stem_conv_fwd(const uint16_t* xsp, const uint16_t* wsp, uint16_t* y,
 // fragments; the block's partial dW leaves once, at the end (fp32 atomics, or a private slab
 // reduced in fixed order for deterministic runs).  Replaces pool_bn_bwd_apply (writes dy, 411 MB
 // at batch 256) + the generic TN weight gradient (reads it back).
+// Pipelining: the next item's raw loads (y, argmax, pooled gradient: registers) and its halo
+// (asm LDS-DMA into the other of two halo buffers) are issued before this item's MFMAs, and the
+// BN coefficients live in LDS to leave registers for that prefetch: 320 -> 297 us at batch 256
+// (scripts/bench_stem_bwd.py); the rest is the dy phase's VALU work (~15 ops per element).
 namespace {
 
 constexpr int SB_THREADS = 256;
@@ -336,6 +340,51 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+
+// Raw loads of one dy unit (quad b of the item's row pair x channel group c8): the 4 y vectors and
+// the 4 covering pooled windows' (argmax, gradient).  Issued one item ahead (into registers) so
+// their latency hides behind the previous item's MFMAs; windows past the pooled edge load the
+// quad's own window (a valid address) and are masked at use.
+struct SbRaw {
+  uint4 y[4];
+  uint2 id[4];
+  uint4 g[4];
+};
+
+__device__ __forceinline__ void sb_load(const StemBwdArgs& P, int n, int a, int b, int c8, SbRaw& r) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    r.y[e] = P.y[((int64_t)(n * P.Ho + 2 * a + (e >> 1)) * P.Wo + 2 * b + (e & 1)) * 8 + c8];
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    const int ho = a + (wi >> 1), wo = b + (wi & 1);
+    const bool ok = ho < P.Hq && wo < P.Wq;
+    const int64_t o = (((int64_t)n * P.Hq + (ok ? ho : a)) * P.Wq + (ok ? wo : b)) * 8 + c8;
+    r.id[wi] = P.idx[o];
+    r.g[wi] = P.dp[o];
+  }
+}
+
+// Opaque use of the prefetched registers at the start of the dy phase: everything computed from
+// them depends on these asm outputs, so the compiler cannot hoist that work (and its vmcnt wait)
+// above the item's barrier into the MFMA loop, where it would stall on the prefetch.
+__device__ __forceinline__ void sb_pin(SbRaw& r) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    asm volatile("" : "+v"(r.y[e].x), "+v"(r.y[e].y), "+v"(r.y[e].z), "+v"(r.y[e].w));
+    asm volatile("" : "+v"(r.g[e].x), "+v"(r.g[e].y), "+v"(r.g[e].z), "+v"(r.g[e].w));
+    asm volatile("" : "+v"(r.id[e].x), "+v"(r.id[e].y));
+  }
+}
+
+// asm LDS-DMA (16 B per lane): invisible to the compiler's waitcnt pass, which would otherwise put a
+// vmcnt(0) -- draining the register prefetch -- in front of every LDS read after it; ordered by the
+// kernel's own vmcnt(0) + barrier
+__device__ __forceinline__ void sb_glds16(const v4i& r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds"
+               :: "v"(voff), "s"(__builtin_amdgcn_readfirstlane(lds)), "s"(r) : "memory", "m0");
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const StemBwdArgs P) {
@@ -343,28 +392,20 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
   const int t = threadIdx.x;
   const int lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
   char* Ds = smem;                       // dy tile [2*Wo][64] bf16
-  char* Hs = smem + 2 * P.Wo * 128;      // 9 input rows
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(P.xsp, P.xsp_bytes);
+  char* Hs0 = smem + 2 * P.Wo * 128;     // 9 input rows, double-buffered (item parity)
+  const uint64_t xa = reinterpret_cast<uint64_t>(P.xsp);
+  const v4i rx = v4i{(int)(uint32_t)xa, (int)((uint32_t)(xa >> 32) & 0xffffu), (int)P.xsp_bytes, 0x00020000};
 
-  // per-thread BN-backward coefficients of its fixed 8-channel group (256 % 8 == 0)
-  const int c8 = t & 7;
-  float k1[8], sgm[8], k2[8], mu[8], sc[8], sh[8];
-  {
-    float is[8], gm[8], s0[8], s1[8];
-    ld8f(P.stats + 64 + c8 * 8, is);
-    ld8f(P.gamma + c8 * 8, gm);
-    ld8f(P.stats + c8 * 8, mu);
-    ld8f(P.sums + c8 * 8, s0);
-    ld8f(P.sums + 64 + c8 * 8, s1);
-    ld8f(P.stats + 128 + c8 * 8, sc);
-    ld8f(P.stats + 192 + c8 * 8, sh);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      k1[j] = gm[j] * is[j];
-      sgm[j] = s0[j] * P.invM;
-      k2[j] = s1[j] * is[j] * is[j] * P.invM;
-    }
+  // BN-backward coefficients per channel in LDS (cf[64][8]: k1, sum g / M, k2, mean, scale, shift),
+  // read per channel inside the dy loop: registers go to the one-item-ahead prefetch instead
+  float* cf = reinterpret_cast<float*>(Hs0 + 2 * P.halo_alloc);
+  if (t < 64) {
+    const float is = P.stats[64 + t];
+    float4* o = reinterpret_cast<float4*>(cf + t * 8);
+    o[0] = make_float4(P.gamma[t] * is, P.sums[t] * P.invM, P.sums[64 + t] * is * is * P.invM, P.stats[t]);
+    o[1] = make_float4(P.stats[128 + t], P.stats[192 + t], 0.f, 0.f);
   }
+  const int c8 = t & 7;  // this thread's fixed 8-channel group (256 % 8 == 0)
 
   const int li = lane & 15, g = lane >> 4;
   const int tq = li >> 2, tp = li & 3;
@@ -377,42 +418,102 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
 
   const int hq2 = P.Ho >> 1;
   const int npx = 2 * P.Wo;
-  for (int item = blockIdx.x; item < P.items; item += gridDim.x) {
-    const int n = item / hq2, a = item - n * hq2;
-    // 1. halo: input rows 4a .. 4a + 8 of image n
-    {
-      const int rows = min(9, P.Hp - 4 * a);
-      const uint32_t span = (uint32_t)rows * P.Wsp * 16;
-      const uint32_t src0 = ((uint32_t)(n * P.Hp + 4 * a) * P.Wsp) * 16;
-      for (int q = wid; q * 1024 < P.halo_alloc; q += SB_THREADS / 64) {
-        const uint32_t o = (uint32_t)q * 1024 + lane * 16;
-        glds16(rx, Hs + q * 1024, o < span ? src0 + o : OOB);
+  const int nu = P.Wq * 8;  // dy units of an item (<= 512: at most two per thread)
+  const bool v0 = t < nu, v1 = t + SB_THREADS < nu;
+  const int b0 = v0 ? t >> 3 : 0, b1 = v1 ? (t + SB_THREADS) >> 3 : 0;
+
+  // halo of item `it` (input rows 4a .. 4a + 8 of image n) into buffer `buf`
+  auto halo = [&](int it, int buf) {
+    const int n = it / hq2, a = it - n * hq2;
+    const int rows = min(9, P.Hp - 4 * a);
+    const uint32_t span = (uint32_t)rows * P.Wsp * 16;
+    const uint32_t src0 = ((uint32_t)(n * P.Hp + 4 * a) * P.Wsp) * 16;
+    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(Hs0 + buf * P.halo_alloc);
+    for (int q = wid; q * 1024 < P.halo_alloc; q += SB_THREADS / 64) {
+      const uint32_t o = (uint32_t)q * 1024 + lane * 16;
+      sb_glds16(rx, dst + q * 1024, o < span ? src0 + o : OOB);
+    }
+  };
+  SbRaw r0, r1;  // raw loads of the item after the current one (two dy units per thread)
+  auto prefetch = [&](int it) {
+    const int n = it / hq2, a = it - n * hq2;
+    sb_load(P, n, a, b0, c8, r0);  // both units unconditionally (b1 clamped): every prefetched
+    sb_load(P, n, a, b1, c8, r1);  // register is consumed each item, so no stale-load wait
+  };
+  // dy of unit (a, b) from its raw loads -> LDS.  The pool gather is pool_grad_quad_regs evaluated
+  // per channel (same sums, same order) so no unpacked quad is held: channel j of the four pixels
+  // is built, BN-applied and packed before channel j + 1.
+  auto dy_unit = [&](const SbRaw& r, int a, int b, bool store) {
+    uint32_t sel[4][2];  // argmax byte words of the four windows; 0xff.. = past the pooled edge
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const bool ok = a + (wi >> 1) < P.Hq && b + (wi & 1) < P.Wq;
+      sel[wi][0] = ok ? r.id[wi].x : 0xffffffffu;
+      sel[wi][1] = ok ? r.id[wi].y : 0xffffffffu;
+    }
+    uint32_t ow[4][4];  // packed bf16 output words: pixel e, channel pair
+    float lo[4];        // pixel e's even channel, waiting for its pair
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 ca = *reinterpret_cast<const float4*>(cf + (c8 * 8 + j) * 8);
+      const float2 cb = *reinterpret_cast<const float2*>(cf + (c8 * 8 + j) * 8 + 4);
+      auto gv = [&](const uint4& v) {
+        const uint32_t w = (&v.x)[j >> 1];
+        return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
+      };
+      uint32_t sb[4];
+#pragma unroll
+      for (int wi = 0; wi < 4; ++wi) sb[wi] = (sel[wi][j >> 2] >> (8 * (j & 3))) & 0xffu;
+      const float g00 = gv(r.g[0]), g01 = gv(r.g[1]), g10 = gv(r.g[2]), g11 = gv(r.g[3]);
+      float pg[4];
+      pg[0] = sb[0] == 4u ? g00 : 0.f;
+      pg[1] = (sb[0] == 5u ? g00 : 0.f) + (sb[1] == 3u ? g01 : 0.f);
+      pg[2] = (sb[0] == 7u ? g00 : 0.f) + (sb[2] == 1u ? g10 : 0.f);
+      pg[3] = ((sb[0] == 8u ? g00 : 0.f) + (sb[1] == 6u ? g01 : 0.f)) +
+              ((sb[2] == 2u ? g10 : 0.f) + (sb[3] == 0u ? g11 : 0.f));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float yy = gv(r.y[e]);
+        const float gr = fmaf(yy, cb.x, cb.y) > 0.f ? pg[e] : 0.f;
+        const float o = P.train ? ca.x * (gr - ca.y - (yy - ca.w) * ca.z) : ca.x * gr;
+        if (j & 1) ow[e][j >> 1] = pack2bf(lo[e], o);
+        else lo[e] = o;
       }
     }
-    // 2. dy of the row pair (2a, 2a + 1): quad (a, b) x channel group c8 per unit
-    for (int u = t; u < P.Wq * 8; u += SB_THREADS) {
-      const int b = u >> 3;
-      uint4 yv[4];  // issued before the argmax gather: independent of it (one round trip, not two)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        yv[e] = P.y[((int64_t)(n * P.Ho + 2 * a + (e >> 1)) * P.Wo + 2 * b + (e & 1)) * 8 + c8];
-      const PoolQuad pq = pool_grad_quad(P.dp, P.idx, n, a, b, c8, 8, P.Hq, P.Wq);
+    if (store) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int hh = e >> 1, w = 2 * b + (e & 1);
-        const f8 yy = unpack8(yv[e]);
-        f8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float gr = fmaf(yy.v[j], sc[j], sh[j]) > 0.f ? pq.g[e].v[j] : 0.f;
-          o.v[j] = P.train ? k1[j] * (gr - sgm[j] - (yy.v[j] - mu[j]) * k2[j]) : k1[j] * gr;
-        }
-        *reinterpret_cast<uint4*>(Ds + swz_tr128(hh * P.Wo + w, c8)) = pack8(o);
+        *reinterpret_cast<uint4*>(Ds + swz_tr128(hh * P.Wo + w, c8)) = make_uint4(ow[e][0], ow[e][1], ow[e][2], ow[e][3]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  };
+
+  __syncthreads();  // cf written
+  // The pass with cur < 0 only issues the block's first item: every prefetch has ONE load site, so
+  // the loop-carried registers need no copies (a copy would wait on the loads it copies).
+  int par = 1;
+  for (int cur = (int)blockIdx.x - (int)gridDim.x; cur < P.items; cur += gridDim.x, par ^= 1) {
+    const bool live = cur >= 0;
+    if (live) {
+      const int a = cur - (cur / hq2) * hq2;
+      // 1. dy of the row pair (2a, 2a + 1) from the prefetched loads
+      sb_pin(r0);
+      dy_unit(r0, a, b0, v0);
+      sb_pin(r1);
+      dy_unit(r1, a, b1, v1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's halo (asm DMA) landed
+      __syncthreads();
+    }
+    // 2. next item's raw loads and halo in flight under this item's MFMAs
+    // (the loads unconditionally -- clamped to the last item when there is no next one -- so the
+    // loop-carried registers have no "kept old value" path, whose copies would wait on them)
+    const int nxt = cur + gridDim.x;
+    prefetch(min(nxt, P.items - 1));
+    if (nxt < P.items) halo(nxt, par ^ 1);
+    if (!live) continue;
     // 3. dW += dy^T x im2col over the pair's pixels, 32 per K-step
+    const char* Hs = Hs0 + par * P.halo_alloc;
     for (int s = 0; s < npx / 32; ++s) {
       const int p0 = s * 32 + 8 * g;           // this lane group's 8 pixels (one row: Wo % 16 == 0)
       const int hh = p0 >= P.Wo ? 1 : 0;
@@ -435,7 +536,9 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) acc[im][jj] = mfma16(af[im], bf[jj], acc[im][jj]);
     }
-    __syncthreads();  // every wave done reading before the next item overwrites the tiles
+    // every wave's LDS reads retired before the next item overwrites Ds / this halo buffer; no
+    // vmcnt here (the prefetch stays in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // partial dW out: lane (fr = li, fq = g) of acc[im][jj] = row im*16 + g*4 + e, column jn*16 + li
@@ -468,7 +571,7 @@ bool stem_bwd_fused_supported(int K, int R, int Sp, int Ho, int Wo) {
   return K == STEM_K && R == STEM_R && Sp == STEM_SP && Ho % 2 == 0 && Wo % 16 == 0 && Wo >= 16 && Wo <= 128;
 }
 
-int stem_bwd_fused_blocks(int N, int Ho) {  // 3 resident blocks per CU (45 KB LDS each)
+int stem_bwd_fused_blocks(int N, int Ho) {  // 2 resident blocks per CU (62 KB LDS each at 224 px)
   return std::max(1, std::min(N * Ho / 2, 512));
 }
 
@@ -494,7 +597,7 @@ void launch_stem_bwd_fused(const uint16_t* dpool, const uint8_t* idx, const uint
   a.slab = ws != nullptr ? 1 : 0;
   a.out = ws != nullptr ? ws : dwsp;
   if (!a.slab) hipMemsetAsync(dwsp, 0, 64 * SB_COLS * sizeof(float), st);
-  const int smem = 2 * Wo * 128 + a.halo_alloc;
+  const int smem = 2 * Wo * 128 + 2 * a.halo_alloc + 64 * 8 * 4;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)stem_bwd_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -902,7 +902,9 @@ def test_stem_halo_conv_vs_fp32(gpu, native_ext, n, h, w):
 
 
 @pytest.mark.parametrize("det", [False, True])
-@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 64, 96)])
+# 24 x 224 and 40 x 64x96: more items than the 512 workgroups, so the next item's halo and raw
+# loads are prefetched under the current item's MFMAs (both halo buffers in use)
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 64, 96), (24, 224, 224), (40, 64, 96)])
 def test_stem_bwd_fused_matches_unfused(gpu, native_ext, n, h, w, det):
     """Fused stem backward (BN/pool apply inside the weight gradient, csrc/kernels/stem.hip) vs the
     unfused pool_bn_bwd_apply + stem_wgrad on identical inputs (same bf16 dy values, different
