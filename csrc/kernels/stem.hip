@@ -293,8 +293,9 @@ void launch_stem_conv_fwd(const uint16_t* xsp, const uint16_t* wsp, uint16_t* y,
 // at batch 256) + the generic TN weight gradient (reads it back).
 // Pipelining: the next item's raw loads (y, argmax, pooled gradient: registers) and its halo
 // (asm LDS-DMA into the other of two halo buffers) are issued before this item's MFMAs, and the
-// BN coefficients live in LDS to leave registers for that prefetch: 320 -> 297 us at batch 256
-// (scripts/bench_stem_bwd.py); the rest is the dy phase's VALU work (~15 ops per element).
+// BN coefficients live in LDS to leave registers for that prefetch, and dy = k1 g + (A y + B) is
+// two FMAs per element: 320 -> 279 us at batch 256
+// (scripts/bench_stem_bwd.py); the rest is mostly the dy phase VALU work (pool gather selects).
 namespace {
 
 constexpr int SB_THREADS = 256;
@@ -396,14 +397,18 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
   const uint64_t xa = reinterpret_cast<uint64_t>(P.xsp);
   const v4i rx = v4i{(int)(uint32_t)xa, (int)((uint32_t)(xa >> 32) & 0xffffu), (int)P.xsp_bytes, 0x00020000};
 
-  // BN-backward coefficients per channel in LDS (cf[64][8]: k1, sum g / M, k2, mean, scale, shift),
-  // read per channel inside the dy loop: registers go to the one-item-ahead prefetch instead
+  // BN-backward coefficients per channel in LDS (cf[64][8]: k1, A, B, scale, shift), read per
+  // channel inside the dy loop (registers go to the one-item-ahead prefetch instead).  Training:
+  // dy = k1 * (g - s0/M - (y - mean) * k2) = k1 * g + (A * y + B), A = -k1 k2, B = k1 (mean k2 - s0/M);
+  // eval: dy = k1 * g (A = B = 0).
   float* cf = reinterpret_cast<float*>(Hs0 + 2 * P.halo_alloc);
   if (t < 64) {
-    const float is = P.stats[64 + t];
+    const float is = P.stats[64 + t], k1 = P.gamma[t] * is;
+    const float k2 = P.train ? P.sums[64 + t] * is * is * P.invM : 0.f;
+    const float sg = P.train ? P.sums[t] * P.invM : 0.f;
     float4* o = reinterpret_cast<float4*>(cf + t * 8);
-    o[0] = make_float4(P.gamma[t] * is, P.sums[t] * P.invM, P.sums[64 + t] * is * is * P.invM, P.stats[t]);
-    o[1] = make_float4(P.stats[128 + t], P.stats[192 + t], 0.f, 0.f);
+    o[0] = make_float4(k1, -k1 * k2, k1 * (P.stats[t] * k2 - sg), P.stats[128 + t]);
+    o[1] = make_float4(P.stats[192 + t], 0.f, 0.f, 0.f);
   }
   const int c8 = t & 7;  // this thread's fixed 8-channel group (256 % 8 == 0)
 
@@ -455,8 +460,8 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
     float lo[4];        // pixel e's even channel, waiting for its pair
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float4 ca = *reinterpret_cast<const float4*>(cf + (c8 * 8 + j) * 8);
-      const float2 cb = *reinterpret_cast<const float2*>(cf + (c8 * 8 + j) * 8 + 4);
+      const float4 ca = *reinterpret_cast<const float4*>(cf + (c8 * 8 + j) * 8);  // k1, A, B, scale
+      const float sft = cf[(c8 * 8 + j) * 8 + 4];
       auto gv = [&](const uint4& v) {
         const uint32_t w = (&v.x)[j >> 1];
         return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
@@ -474,8 +479,8 @@ __global__ void __launch_bounds__(SB_THREADS, 2) stem_bwd_fused_kernel(const Ste
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float yy = gv(r.y[e]);
-        const float gr = fmaf(yy, cb.x, cb.y) > 0.f ? pg[e] : 0.f;
-        const float o = P.train ? ca.x * (gr - ca.y - (yy - ca.w) * ca.z) : ca.x * gr;
+        const float gr = fmaf(yy, ca.w, sft) > 0.f ? pg[e] : 0.f;
+        const float o = fmaf(ca.x, gr, fmaf(ca.y, yy, ca.z));
         if (j & 1) ow[e][j >> 1] = pack2bf(lo[e], o);
         else lo[e] = o;
       }
