@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--fp8-parts", default="all", choices=["all", "fwd", "fwd+dgrad"],
                     help="diagnostics: which GEMMs take fp8 (forward only / + input gradients / + weight "
                          "gradients)")
+    ap.add_argument("--repeats", type=int, default=1,
+                    help="native runs from the same init and data order (stock runs once); the JSON's "
+                         "native curve is their mean, the single runs are listed too")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.fp8:
@@ -74,32 +77,44 @@ def main():
     ds = learnable_dataset(a.samples, a.image, a.classes, device=dev, seed=3, noise=a.noise)
     torch.manual_seed(0)
     stock = build_model(a.arch, num_classes=a.classes).to(dev)
-    native_m = copy.deepcopy(stock).set_impl("native")
-    native = DistributedDataParallel(native_m)          # world 1: flat space + grad sinks
-    opt_n = SGD(native.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
+    init = copy.deepcopy(stock)
+
+    def batches():
+        g = torch.Generator().manual_seed(11)
+        perm = torch.randperm(len(ds), generator=g).to(dev)
+        pos = 0
+        for _ in range(a.steps):
+            if pos + a.batch > len(ds):
+                perm = torch.randperm(len(ds), generator=g).to(dev)
+                pos = 0
+            idx = perm[pos:pos + a.batch]
+            pos += a.batch
+            yield ds.images[idx], ds.labels[idx]
+
+    runs, accs = [], []
+    for _ in range(a.repeats):
+        native_m = copy.deepcopy(init).set_impl("native")
+        native = DistributedDataParallel(native_m)          # world 1: flat space + grad sinks
+        opt_n = SGD(native.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
+        ln = []
+        for x, y in batches():
+            opt_n.zero_grad()
+            loss_n = ops.cross_entropy(native(x), y)
+            loss_n.backward()
+            opt_n.step()
+            ln.append(loss_n.detach())
+        runs.append(torch.stack(ln).float().cpu())
+        accs.append(accuracy(native, ds, True))
+        del native, native_m, opt_n
     opt_s = torch.optim.SGD(stock.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-5)
-    g = torch.Generator().manual_seed(11)
-    perm = torch.randperm(len(ds), generator=g).to(dev)
-    pos = 0
-    ln, ls = [], []
-    for step in range(a.steps):
-        if pos + a.batch > len(ds):
-            perm = torch.randperm(len(ds), generator=g).to(dev)
-            pos = 0
-        idx = perm[pos:pos + a.batch]
-        pos += a.batch
-        x, y = ds.images[idx], ds.labels[idx]
-        opt_n.zero_grad()
-        loss_n = ops.cross_entropy(native(x), y)
-        loss_n.backward()
-        opt_n.step()
+    ls = []
+    for x, y in batches():
         opt_s.zero_grad()
         loss_s = F.cross_entropy(stock(x), y)
         loss_s.backward()
         opt_s.step()
-        ln.append(loss_n.detach())
         ls.append(loss_s.detach())
-    ln = torch.stack(ln).float().cpu()
+    ln = torch.stack(runs).mean(0)
     ls = torch.stack(ls).float().cpu()
     w = a.window
     nwin = a.steps // w
@@ -109,9 +124,13 @@ def main():
         "window": w,
         "native_window_loss": [round(float(ln[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],
         "stock_window_loss": [round(float(ls[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)],
-        "native_train_acc": accuracy(native, ds, True),
+        "native_train_acc": min(accs),
+        "native_train_accs": accs,
+        "native_window_loss_runs": [[round(float(r[i * w:(i + 1) * w].mean()), 4) for i in range(nwin)]
+                                    for r in runs],
         "stock_train_acc": accuracy(stock, ds, False),
-        "finite": bool(torch.isfinite(ln).all() and torch.isfinite(ls).all()),
+        "finite": bool(all(torch.isfinite(r).all() for r in runs) and torch.isfinite(ls).all()),
+        "repeats": a.repeats,
     }
     line = json.dumps(res)
     print(line, flush=True)
