@@ -71,19 +71,24 @@ def critical_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
 
 
 def critical_priority_wanted(collective: bool, graph: bool) -> bool:
-    """Whether the step should run on :func:`critical_stream`.
+    """Whether the step should run on :func:`critical_stream` (``collective`` / ``graph``: the
+    step's kind, kept for callers; the answer no longer depends on it).
 
-    Only for an eager step with no gradient collectives.  The priority pays in the plain
+    History: the priority paid in the plain
     single-GPU step (r3z, same box: 19.41 -> 18.95 ms) but costs far more than it gains as soon
     as the step adds cross-stream synchronisation with a normal-priority stream outside the
     compute chain: ResNet-50 with the gradient reducer (world-1 RCCL or xGMI) 19.5 -> 28.4 ms,
     its HIP-graph replay 20.7 -> 29.6 ms, ResNet-18/CIFAR graph replay 2.04 -> 6.34 ms; every
     small main-stream kernel is ~35 us longer in the kernel trace
-    (``profiles/r3z_priority_vs_sync.md``).  ``PDT_MAIN_PRIO=1`` / ``=0`` forces it on / off."""
-    e = os.environ.get("PDT_MAIN_PRIO", "auto")
-    if e in ("0", "1"):
-        return e == "1"
-    return not collective and not graph
+    (``profiles/r3z_priority_vs_sync.md``).
+
+    Off by default since round 5: with the BN backward folded into the input gradient and the
+    forward statistics taken in the conv epilogue, the plain step is FASTER at normal priority
+    (r7q, same call, two runs each: 18.11 / 18.08 ms vs 18.22 / 18.16 ms with the priority), and
+    the N>1 code path at world 1 (``--force-comm``, normal priority) is within 0.2 % of either
+    (RCCL 18.26 / 18.20, xGMI 18.16 / 18.15; ``profiles/r7q_priority_ab.jsonl``).  So every world
+    size now runs the same stream setup.  ``PDT_MAIN_PRIO=1`` forces the priority on."""
+    return os.environ.get("PDT_MAIN_PRIO", "0") == "1"
 
 
 def use_critical_stream(device: torch.device, collective: bool = False,

@@ -343,11 +343,11 @@ def test_auto_last_bucket_cap_from_tail_model():
 
 
 def test_critical_priority_policy(monkeypatch):
-    """High-priority critical stream only for an eager step without gradient collectives
-    (profiles/r3z_priority_vs_sync.md); PDT_MAIN_PRIO forces it either way."""
+    """Normal priority everywhere by default since round 5 (profiles/r7q_priority_ab.jsonl: the
+    plain step is faster without it and the N>1 path matches it); PDT_MAIN_PRIO=1 forces it on."""
     from pytorch_distributed_tutorials_amd.ops import streams
     monkeypatch.delenv("PDT_MAIN_PRIO", raising=False)
-    assert streams.critical_priority_wanted(collective=False, graph=False)
+    assert not streams.critical_priority_wanted(collective=False, graph=False)
     assert not streams.critical_priority_wanted(collective=True, graph=False)
     assert not streams.critical_priority_wanted(collective=False, graph=True)
     monkeypatch.setenv("PDT_MAIN_PRIO", "0")
