@@ -237,14 +237,22 @@ __global__ void __launch_bounds__(256) bn_finalize_sums_kernel(double* __restric
                                                                float eps, float* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
+  // every load issued up front: one memory round trip on the critical stream, not two
+  double s[kStatSlots], q[kStatSlots];
+#pragma unroll
+  for (int x = 0; x < kStatSlots; ++x) {  // the conv's per-XCD slots
+    s[x] = acc[(size_t)x * 2 * K + k];
+    q[x] = acc[(size_t)x * 2 * K + K + k];
+  }
+  const float g = gamma[k], bt = beta[k];
+  const float rm0 = rm != nullptr ? rm[k] : 0.f, rv0 = rm != nullptr ? rv[k] : 0.f;
   double S = 0.0, Q = 0.0;
 #pragma unroll
-  for (int x = 0; x < kStatSlots; ++x) {  // the conv's per-XCD slots, fixed order
-    double* a = acc + (size_t)x * 2 * K;
-    S += a[k];
-    Q += a[K + k];
-    a[k] = 0.0;
-    a[K + k] = 0.0;
+  for (int x = 0; x < kStatSlots; ++x) {  // fixed order
+    S += s[x];
+    Q += q[x];
+    acc[(size_t)x * 2 * K + k] = 0.0;
+    acc[(size_t)x * 2 * K + K + k] = 0.0;
   }
   const double Md = (double)M;
   const double mu = S / Md;
@@ -252,14 +260,14 @@ __global__ void __launch_bounds__(256) bn_finalize_sums_kernel(double* __restric
   const float invstd = rsqrtf((float)var + eps);
   if (rm != nullptr) {
     const float unb = M > 1 ? (float)(var * Md / (Md - 1.0)) : (float)var;
-    rm[k] = (1.f - momentum) * rm[k] + momentum * (float)mu;
-    rv[k] = (1.f - momentum) * rv[k] + momentum * unb;
+    rm[k] = (1.f - momentum) * rm0 + momentum * (float)mu;
+    rv[k] = (1.f - momentum) * rv0 + momentum * unb;
   }
-  const float sc = gamma[k] * invstd;
+  const float sc = g * invstd;
   out[k] = (float)mu;
   out[K + k] = invstd;
   out[2 * K + k] = sc;
-  out[3 * K + k] = beta[k] - (float)mu * sc;
+  out[3 * K + k] = bt - (float)mu * sc;
 }
 
 void launch_bn_finalize_sums(const BnFwdFuse& bn, int M, int K, hipStream_t st) {
