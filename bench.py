@@ -164,7 +164,7 @@ def main(argv=None) -> int:
         if args.impl == "native":
             from pytorch_distributed_tutorials_amd.ops.streams import use_critical_stream
             use_critical_stream(torch.device("cuda", dev_index), collective=world > 1 or args.force_comm,
-                                graph=args.graph)
+                                graph=args.graph, fp8=args.fp8)
     dev = torch.device(f"cuda:{dev_index}" if torch.cuda.is_available() else "cpu")
     dev_ids = [dev_index] if dev.type == "cuda" else None
     torch.manual_seed(0)

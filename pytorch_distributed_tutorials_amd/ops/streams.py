@@ -70,9 +70,10 @@ def critical_stream(device: torch.device) -> Optional[torch.cuda.Stream]:
     return s
 
 
-def critical_priority_wanted(collective: bool, graph: bool) -> bool:
-    """Whether the step should run on :func:`critical_stream` (``collective`` / ``graph``: the
-    step's kind, kept for callers; the answer no longer depends on it).
+def critical_priority_wanted(collective: bool, graph: bool, fp8: bool = False) -> bool:
+    """Whether the step should run on :func:`critical_stream`: the eager fp8 step without gradient
+    collectives (r7x, same call: 16.66 / 16.66 ms with the priority vs 16.96 / 16.91 without);
+    nothing else (below).
 
     History: the priority paid in the plain
     single-GPU step (r3z, same box: 19.41 -> 18.95 ms) but costs far more than it gains as soon
@@ -87,16 +88,19 @@ def critical_priority_wanted(collective: bool, graph: bool) -> bool:
     (r7q, same call, two runs each: 18.11 / 18.08 ms vs 18.22 / 18.16 ms with the priority), and
     the N>1 code path at world 1 (``--force-comm``, normal priority) is within 0.2 % of either
     (RCCL 18.26 / 18.20, xGMI 18.16 / 18.15; ``profiles/r7q_priority_ab.jsonl``).  So every world
-    size now runs the same stream setup.  ``PDT_MAIN_PRIO=1`` forces the priority on."""
-    return os.environ.get("PDT_MAIN_PRIO", "0") == "1"
+    size now runs the same stream setup.  ``PDT_MAIN_PRIO=1`` / ``=0`` forces it on / off."""
+    e = os.environ.get("PDT_MAIN_PRIO", "auto")
+    if e in ("0", "1"):
+        return e == "1"
+    return fp8 and not collective and not graph
 
 
 def use_critical_stream(device: torch.device, collective: bool = False,
-                        graph: bool = False) -> Optional[torch.cuda.Stream]:
+                        graph: bool = False, fp8: bool = False) -> Optional[torch.cuda.Stream]:
     """Make :func:`critical_stream` the current stream of ``device`` when
     :func:`critical_priority_wanted` says so (call once, before the model and its buffers are
     touched, so every later op orders on it)."""
-    if not critical_priority_wanted(collective, graph):
+    if not critical_priority_wanted(collective, graph, fp8):
         return None
     s = critical_stream(device)
     if s is not None:

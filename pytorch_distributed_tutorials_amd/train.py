@@ -207,8 +207,8 @@ def main(argv: Optional[list] = None) -> int:
     if impl == "native" and device.type == "cuda":
         torch.cuda.set_device(device)
         from .ops.streams import use_critical_stream
-        # the step's critical path outranks the side streams (eager single-process steps only)
-        use_critical_stream(device, collective=env.world_size > 1, graph=bool(args.graph))
+        # high-priority critical path: eager single-process fp8 steps only (ops/streams.py)
+        use_critical_stream(device, collective=env.world_size > 1, graph=bool(args.graph), fp8=dtype == "fp8")
     autocast = (impl == "torch" and dtype == "bf16")
     if args.trace:
         trace.enable(True)

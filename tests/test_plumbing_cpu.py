@@ -343,13 +343,16 @@ def test_auto_last_bucket_cap_from_tail_model():
 
 
 def test_critical_priority_policy(monkeypatch):
-    """Normal priority everywhere by default since round 5 (profiles/r7q_priority_ab.jsonl: the
-    plain step is faster without it and the N>1 path matches it); PDT_MAIN_PRIO=1 forces it on."""
+    """Normal priority by default since round 5 (profiles/r7q_priority_ab.jsonl: the plain bf16
+    step is faster without it and the N>1 path matches it); only the eager fp8 step without
+    collectives keeps it; PDT_MAIN_PRIO forces it either way."""
     from pytorch_distributed_tutorials_amd.ops import streams
     monkeypatch.delenv("PDT_MAIN_PRIO", raising=False)
     assert not streams.critical_priority_wanted(collective=False, graph=False)
     assert not streams.critical_priority_wanted(collective=True, graph=False)
     assert not streams.critical_priority_wanted(collective=False, graph=True)
+    assert streams.critical_priority_wanted(collective=False, graph=False, fp8=True)
+    assert not streams.critical_priority_wanted(collective=True, graph=False, fp8=True)
     monkeypatch.setenv("PDT_MAIN_PRIO", "0")
     assert not streams.critical_priority_wanted(collective=False, graph=False)
     monkeypatch.setenv("PDT_MAIN_PRIO", "1")
