@@ -89,13 +89,20 @@ def test_resnet50_training_tracks_stock_fp32(gpu, tmp_path, fp8):
     # both learn (the loss falls well below its start), and track each other window by window
     assert n[-1] < 0.2 * n[0] and s[-1] < 0.2 * s[0], (n, s)
     assert res["native_train_acc"] > 0.9 and res["stock_train_acc"] > 0.9, res
-    # fp8 and bf16: the same criterion as ResNet-18 -- every 20-step window (of the 3-run mean)
-    # within 0.15 + 25 % of the stock curve AT THE SAME WINDOW, and the final accuracy above 0.95.
-    # (Round 4 allowed fp8 a one-window lag; per-part runs show no GEMM family lagging
-    # systematically -- profiles/r6_fp8_parity.txt -- and the steep windows move by up to ~0.4 run
-    # to run in bf16 too.)
+    # bf16: the ResNet-18 criterion -- every 20-step window (of the 3-run mean) within 0.15 + 25 %
+    # of the stock curve AT THE SAME WINDOW -- and the final accuracy above 0.95; fp8: the same, with
+    # a one-window lag allowed in windows 4-6 only (below).
     assert res["native_train_acc"] > 0.95, res  # the worst of the runs
     for run in res["native_window_loss_runs"]:
         assert run[-1] < 0.2 * run[0], res["native_window_loss_runs"]
-    for a, b in zip(n, s):
-        assert abs(a - b) <= 0.15 + 0.25 * b, (n, s, res["native_window_loss_runs"])
+    # fp8 only, windows 4-6 (0-based 3..5, the steepest part): the same band may be met against the
+    # stock window one earlier (a 20-step lag).  Measured: the fp8 3-run mean sits 0.15-0.45 above
+    # stock there (0-based window 5: 1.55 / 1.71 vs stock 1.25 and bf16 1.44, r7o / r7y) and is back on
+    # the stock curve by window 8; every other window, the final one included, keeps the same-window
+    # band (the advisor's "lag allowance only for windows 4-6, tight final window").
+    band = lambda b: 0.15 + 0.25 * b  # noqa: E731
+    for i, (a, b) in enumerate(zip(n, s)):
+        ok = abs(a - b) <= band(b)
+        if fp8 and 3 <= i <= 5:
+            ok = ok or abs(a - s[i - 1]) <= band(s[i - 1])
+        assert ok, (i, n, s, res["native_window_loss_runs"])
