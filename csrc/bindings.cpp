@@ -325,27 +325,41 @@ static std::pair<float*, float*> bn_param_sinks(const std::optional<Tensor>& dga
                                                 const std::optional<Tensor>& dbeta, int64_t K);
 
 // Weight gradient of a folded unit (kernels.h launch_bn_fold_wgrad): out [K,C,1,1] fp32 (a KRSC-dense
-// view, e.g. the flat gradient buffer) += diag(k1) t1 + diag(a) w gram + b colsum^T; dgamma/dbeta
-// (optional) take the BN parameter gradients.
-void bn_fold_wgrad(const Tensor& t1, const Tensor& gram, const Tensor& colsum, const Tensor& w,
+// view, e.g. the flat gradient buffer) += diag(k1) t1 + diag(a) W gram + b colsum^T with W the bf16
+// mirror wt [C][K] (the operand bn_fold_weights read); dgamma/dbeta (optional) take the BN parameter
+// gradients.  done (an int32 [1] counter, 0 between calls): consume mode -- t1 and gram are persistent
+// workspaces the kernel clears after reading, and `sums` too when zero_sums.
+void bn_fold_wgrad(Tensor t1, Tensor gram, const Tensor& colsum, const Tensor& wt,
                    const Tensor& stats, const Tensor& gamma, const Tensor& sums, int64_t count, Tensor out,
-                   const std::optional<Tensor>& dgamma, const std::optional<Tensor>& dbeta) {
-  const int K = w.size(0), C = w.size(1);
-  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == (int64_t)K * C, "w: fp32 [K, C, 1, 1]");
+                   const std::optional<Tensor>& dgamma, const std::optional<Tensor>& dbeta,
+                   const std::optional<Tensor>& done, bool zero_sums) {
+  check_cuda(wt, "wt");
+  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() == wt.size(0) * wt.size(-1),
+              "wt must be contiguous bf16 [C][K]");
+  const int C = wt.size(0), K = wt.size(-1);
   TORCH_CHECK(t1.scalar_type() == at::kFloat && t1.numel() == (int64_t)K * C, "t1: fp32 [K, C]");
   TORCH_CHECK(gram.scalar_type() == at::kFloat && gram.numel() == (int64_t)C * C, "gram: fp32 [C, C]");
   TORCH_CHECK(colsum.scalar_type() == at::kFloat && colsum.numel() >= C && colsum.is_contiguous(), "colsum: fp32 [C]");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == (int64_t)K * C, "out: fp32 [K, C, 1, 1]");
-  for (const Tensor* x : {&t1, &gram, &w, const_cast<const Tensor*>(&out)}) {
+  for (const Tensor* x : {(const Tensor*)&t1, (const Tensor*)&gram, (const Tensor*)&out}) {
     // 1x1: [K,C,1,1] in either memory format is [K][C] memory when its two big strides are (C, 1)
     TORCH_CHECK(x->stride(0) == x->size(1) && x->stride(1) == 1, "fold wgrad: [K][C]-dense operands");
   }
-  TORCH_CHECK(stats.numel() == 4 * K && gamma.numel() == K && sums.numel() == 2 * K, "BN operands: [4,K], [K], [2,K]");
-  c10::hip::HIPGuard g(w.get_device());
+  TORCH_CHECK(stats.numel() == 4 * K && gamma.numel() == K && sums.numel() == 2 * K && sums.is_contiguous(),
+              "BN operands: [4,K], [K], [2,K]");
+  int* dp = nullptr;
+  if (done.has_value() && done->defined()) {
+    TORCH_CHECK(done->is_cuda() && done->scalar_type() == at::kInt && done->numel() >= C / 64 + 1,
+                "done: int32 device counters [C / 64 + 1]");
+    dp = done->data_ptr<int>();
+  }
+  TORCH_CHECK(!zero_sums || dp != nullptr, "zero_sums needs the completion counter");
+  c10::hip::HIPGuard g(wt.get_device());
   auto pg = bn_param_sinks(dgamma, dbeta, K);
-  pdt::launch_bn_fold_wgrad(t1.data_ptr<float>(), gram.data_ptr<float>(), colsum.data_ptr<float>(), w.data_ptr<float>(),
-                            stats.data_ptr<float>(), gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K,
-                            out.data_ptr<float>(), pg.first, pg.second, cur_stream(w));
+  pdt::launch_bn_fold_wgrad(t1.data_ptr<float>(), gram.data_ptr<float>(), colsum.data_ptr<float>(),
+                            reinterpret_cast<const uint16_t*>(wt.data_ptr()), stats.data_ptr<float>(),
+                            gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K, out.data_ptr<float>(),
+                            pg.first, pg.second, dp, zero_sums, cur_stream(wt));
 }
 
 // BN-fused dgrad of a 1x1 / stride-1 conv with the NEXT unit's BN backward folded in (kernels.h
@@ -1457,8 +1471,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fold_weights", checked("bn_fold_weights", &bn_fold_weights), py::arg("wt"), py::arg("stats"),
         py::arg("gamma"), py::arg("sums"), py::arg("count"));
   m.def("bn_fold_wgrad", checked("bn_fold_wgrad", &bn_fold_wgrad), py::arg("t1"), py::arg("gram"),
-        py::arg("colsum"), py::arg("w"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("count"),
-        py::arg("out"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+        py::arg("colsum"), py::arg("wt"), py::arg("stats"), py::arg("gamma"), py::arg("sums"), py::arg("count"),
+        py::arg("out"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
+        py::arg("done") = py::none(), py::arg("zero_sums") = false);
   m.def("conv_dgrad_bn_fold", checked("conv_dgrad_bn_fold", &conv_dgrad_bn_fold), py::arg("g"), py::arg("z_in"),
         py::arg("wfold"), py::arg("bias"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
         py::arg("acc"));
@@ -1671,5 +1686,16 @@ PYBIND11_MODULE(_C, m) {
       .def("comm_timing", &pdt::Reducer::comm_timing, py::call_guard<py::gil_scoped_release>())
       .def("set_strict", &pdt::Reducer::set_strict)
       .def("set_aux_stream", &pdt::Reducer::set_aux_stream)
-      .def_property_readonly("duplicate_marks", &pdt::Reducer::duplicate_marks);
+      .def_property_readonly("duplicate_marks", &pdt::Reducer::duplicate_marks)
+      .def("set_optimizer", &pdt::Reducer::set_optimizer, py::arg("param_flat"), py::arg("grad_flat"))
+      .def("arm_optimizer", [](pdt::Reducer& r, double lr, double mom, double damp, double wd, bool nest, bool first,
+                               const std::optional<Tensor>& buf, const std::optional<Tensor>& mirror) {
+             r.arm_optimizer(lr, mom, damp, wd, nest, first, buf.has_value() ? *buf : Tensor(),
+                             mirror.has_value() ? *mirror : Tensor());
+           }, py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"),
+           py::arg("nesterov"), py::arg("first"), py::arg("momentum_buf") = py::none(),
+           py::arg("mirror") = py::none())
+      .def("optimizer_applied", &pdt::Reducer::optimizer_applied)
+      .def("consume_optimizer", &pdt::Reducer::consume_optimizer)
+      .def_property_readonly("local", &pdt::Reducer::local);
 }

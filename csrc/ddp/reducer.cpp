@@ -52,6 +52,23 @@ struct ReducerState {
   hipStream_t aux = nullptr;
   hipEvent_t ev_aux = nullptr;
 
+  // LOCAL mode: one process, no communicator -- the optimizer-overlap stream only
+  bool local = false;
+  hipStream_t local_stream = nullptr;
+  hipEvent_t ev_local = nullptr, ev_join = nullptr;
+  // per-bucket fused SGD (optimizer in backward)
+  float* sgd_p = nullptr;
+  const float* grad_base = nullptr;
+  at::Tensor grad_flat;          // for its version counter
+  std::vector<int64_t> goff;     // element offset of each bucket in the flat buffers
+  bool sgd_armed = false;
+  float sgd_lr = 0.f, sgd_mom = 0.f, sgd_damp = 0.f, sgd_wd = 0.f;
+  bool sgd_nest = false, sgd_first = false;
+  float* sgd_buf = nullptr;
+  uint16_t* sgd_pb = nullptr;
+  int64_t sgd_applied = 0;
+  std::pair<int64_t, int64_t> sgd_last{-1, -1};
+
   std::mutex mu;
   bool enabled = true;
   bool expecting = false;
@@ -72,9 +89,29 @@ struct ReducerState {
     launch_order.clear();
   }
 
+  // the fused SGD over bucket b's flat range, on stream s behind its reduction
+  void apply_sgd(int64_t b, hipStream_t s) {
+    if (!sgd_armed) return;
+    const int64_t off = goff[b];
+    launch_sgd(sgd_p + off, grad_base + off, sgd_buf ? sgd_buf + off : nullptr, flats[b].numel(), sgd_lr,
+               sgd_mom, sgd_damp, sgd_wd, sgd_nest, sgd_first, 1.f, s, sgd_pb ? sgd_pb + off : nullptr);
+    ++sgd_applied;
+  }
+
   void launch_bucket(int64_t b) {
     const bool first = launch_order.empty();
     launch_order.push_back(b);
+    if (local) {
+      if (!sgd_armed) return;  // nothing to reduce in one process: only the update runs here
+      const int dev = params[0].get_device();
+      c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
+      hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+      stream_handoff(cur, local_stream, ev_local);
+      if (aux) stream_handoff(aux, local_stream, ev_aux);
+      if (timing && first) hipEventRecord(ev_start, local_stream);
+      apply_sgd(b, local_stream);
+      return;
+    }
     if (xgmi) {
       xgmi->check();  // a peer timed out earlier: raise here, out of backward()
       c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
@@ -84,6 +121,7 @@ struct ReducerState {
       }
       if (timing && first) hipEventRecord(ev_start, xgmi->stream());
       xgmi->reduce_bucket((int)b, flat_off[b], flats[b].numel(), average);
+      apply_sgd(b, xgmi->stream());
       return;
     }
     if (comm) {
@@ -109,6 +147,7 @@ struct ReducerState {
         comm->all_reduce_raw(f.data_ptr(), (size_t)f.numel(), RcclComm::dtype_of(f),
                              average ? ncclAvg : ncclSum);
       }
+      apply_sgd(b, cs);
     } else {
       if (aux) {
         // device gradients through a non-RCCL group (gloo on GPU tensors): the collective runs
@@ -181,7 +220,21 @@ struct ReducerState {
     // parameters that received no gradient this iteration (unused in forward): zero views
     for (size_t i = 0; i < params.size(); ++i)
       if (!param_ready[i]) mark_param((int64_t)i, /*zero_if_missing=*/true);
-    if (xgmi) {
+    if (local) {
+      if (!(sgd_armed && sgd_applied > 0)) {
+        timed = false;
+      } else {
+      const int dev = params[0].get_device();
+      c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
+      hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+      if (timing) {
+        hipEventRecord(ev_bwd, cur);
+        hipEventRecord(ev_end, local_stream);
+        timed = !launch_order.empty();
+      }
+      stream_handoff(local_stream, cur, ev_join);
+      }
+    } else if (xgmi) {
       if (timing) {
         c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
         hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)xgmi->device()).stream();
@@ -204,6 +257,10 @@ struct ReducerState {
       py_finalize();
     }
     last_order = launch_order;
+    if (sgd_armed) {
+      sgd_last = {sgd_applied, grad_flat.defined() ? (int64_t)grad_flat._version() : -1};
+      sgd_armed = false;
+    }
     expecting = false;
     callback_queued = false;
     ++iters;
@@ -234,6 +291,18 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
         throw std::runtime_error("Reducer: bucket is not a slice of the xGMI gradient buffer");
       st_->flat_off.push_back(off);
     }
+  }
+  st_->local = !st_->comm && !st_->xgmi && py_launch.is_none();
+  if (st_->local) {
+    if (st_->params.empty() || !st_->params[0].is_cuda())
+      throw std::runtime_error("Reducer: local mode (no communicator, no Python launch) needs device parameters");
+    c10::hip::HIPGuard guard((c10::DeviceIndex)st_->params[0].get_device());
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&st_->local_stream, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipEventCreateWithFlags(&st_->ev_local, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&st_->ev_join, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("Reducer: local stream / events");
   }
   st_->py_launch = std::move(py_launch);
   st_->py_finalize = std::move(py_finalize);
@@ -274,15 +343,21 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
 }
 
 Reducer::~Reducer() {
-  for (hipEvent_t e : {st_->ev_start, st_->ev_end, st_->ev_bwd, st_->ev_aux})
+  for (hipEvent_t e : {st_->ev_start, st_->ev_end, st_->ev_bwd, st_->ev_aux, st_->ev_local, st_->ev_join})
     if (e) hipEventDestroy(e);
+  if (st_->local_stream) {
+    hipStreamSynchronize(st_->local_stream);
+    hipStreamDestroy(st_->local_stream);
+  }
 }
 
 void Reducer::set_timing(bool on) {
   std::lock_guard<std::mutex> lk(st_->mu);
-  if (on && !st_->comm && !st_->xgmi) throw std::runtime_error("Reducer timing needs a native communicator");
+  if (on && !st_->comm && !st_->xgmi && !st_->local)
+    throw std::runtime_error("Reducer timing needs a native communicator (or local mode)");
   if (on && !st_->ev_start) {
-    c10::hip::HIPGuard guard((c10::DeviceIndex)(st_->comm ? st_->comm->device() : st_->xgmi->device()));
+    c10::hip::HIPGuard guard((c10::DeviceIndex)(st_->comm ? st_->comm->device()
+                                                : st_->xgmi ? st_->xgmi->device() : st_->params[0].get_device()));
     for (hipEvent_t* e : {&st_->ev_start, &st_->ev_end, &st_->ev_bwd})
       if (hipEventCreate(e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
   }
@@ -315,6 +390,56 @@ void Reducer::set_aux_stream(uintptr_t stream) {
   st_->aux = reinterpret_cast<hipStream_t>(stream);
 }
 int64_t Reducer::duplicate_marks() const { return st_->duplicate_marks; }
+
+void Reducer::set_optimizer(const at::Tensor& param_flat, const at::Tensor& grad_flat) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  if (!st_->comm && !st_->xgmi && !st_->local)
+    throw std::runtime_error("Reducer: the optimizer overlap needs a native communicator or local mode");
+  if (!param_flat.is_cuda() || param_flat.scalar_type() != at::kFloat || !param_flat.is_contiguous() ||
+      !grad_flat.is_cuda() || grad_flat.scalar_type() != at::kFloat || !grad_flat.is_contiguous() ||
+      param_flat.numel() != grad_flat.numel())
+    throw std::runtime_error("Reducer::set_optimizer: contiguous fp32 device flat buffers of one size");
+  const float* base = grad_flat.data_ptr<float>();
+  std::vector<int64_t> off;
+  for (const auto& f : st_->flats) {
+    const int64_t o = f.data_ptr<float>() - base;
+    if (o < 0 || o + f.numel() > grad_flat.numel())
+      throw std::runtime_error("Reducer::set_optimizer: a bucket is not a slice of grad_flat");
+    off.push_back(o);
+  }
+  st_->goff = std::move(off);
+  st_->grad_base = base;
+  st_->grad_flat = grad_flat;
+  st_->sgd_p = param_flat.data_ptr<float>();
+}
+
+void Reducer::arm_optimizer(double lr, double momentum, double dampening, double weight_decay, bool nesterov,
+                            bool first, const at::Tensor& momentum_buf, const at::Tensor& mirror_bf16) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  if (!st_->sgd_p) throw std::runtime_error("Reducer::arm_optimizer before set_optimizer");
+  const int64_t n = st_->grad_flat.numel();
+  if (momentum != 0.0 && !(momentum_buf.defined() && momentum_buf.numel() == n &&
+                           momentum_buf.scalar_type() == at::kFloat && momentum_buf.is_contiguous()))
+    throw std::runtime_error("Reducer::arm_optimizer: momentum needs a contiguous fp32 flat buffer");
+  if (mirror_bf16.defined() && (mirror_bf16.numel() != n || mirror_bf16.scalar_type() != at::kBFloat16 ||
+                                !mirror_bf16.is_contiguous()))
+    throw std::runtime_error("Reducer::arm_optimizer: the weight mirror must be a contiguous bf16 flat buffer");
+  st_->sgd_lr = (float)lr;
+  st_->sgd_mom = (float)momentum;
+  st_->sgd_damp = (float)dampening;
+  st_->sgd_wd = (float)weight_decay;
+  st_->sgd_nest = nesterov;
+  st_->sgd_first = first;
+  st_->sgd_buf = momentum != 0.0 ? momentum_buf.data_ptr<float>() : nullptr;
+  st_->sgd_pb = mirror_bf16.defined() ? reinterpret_cast<uint16_t*>(mirror_bf16.data_ptr()) : nullptr;
+  st_->sgd_applied = 0;
+  st_->sgd_armed = true;
+  st_->sgd_last = {-1, -1};
+}
+
+std::pair<int64_t, int64_t> Reducer::optimizer_applied() const { return st_->sgd_last; }
+void Reducer::consume_optimizer() { st_->sgd_last = {-1, -1}; }
+bool Reducer::local() const { return st_->local; }
 
 void Reducer::prepare_for_backward() {
   std::lock_guard<std::mutex> lk(st_->mu);

@@ -19,6 +19,13 @@
 //     stream, zero-fills buckets of parameters that got no gradient, and resets.
 // Non-RCCL process groups (gloo on CPU, used by the tests) plug in via Python
 // launch/finalize callbacks while keeping all the bookkeeping here.
+//
+// Optimizer in backward: with set_optimizer + arm_optimizer, the fused SGD
+// runs over each bucket's flat range right behind that bucket's all-reduce, on the same stream, so
+// only the last bucket's update is left after backward (torch.optim.SGD math, sgd.hip).  In a
+// single process without a communicator the reducer runs in LOCAL mode (py_launch = None): no
+// collective, a private low-priority stream that waits for the compute and weight-gradient streams
+// and runs each bucket's update as soon as its gradients are final.
 #pragma once
 #include <ATen/ATen.h>
 #include <pybind11/pybind11.h>
@@ -64,6 +71,17 @@ class Reducer {
   // bucket all-reduces additionally wait for this stream (gradients produced on a side stream)
   void set_aux_stream(uintptr_t stream);
   int64_t duplicate_marks() const;
+  // per-bucket fused SGD: param_flat / grad_flat are the flat buffers the buckets are slices of
+  void set_optimizer(const at::Tensor& param_flat, const at::Tensor& grad_flat);
+  // arm the update for the next backward (hyperparameters of torch.optim.SGD; momentum_buf and
+  // mirror_bf16 -- the flat bf16 weight mirror the SGD kernel also writes -- may be undefined)
+  void arm_optimizer(double lr, double momentum, double dampening, double weight_decay, bool nesterov,
+                     bool first, const at::Tensor& momentum_buf, const at::Tensor& mirror_bf16);
+  // (buckets updated by the last finished backward, grad_flat's version counter at its end);
+  // (-1, -1) when it applied none or the result was consumed
+  std::pair<int64_t, int64_t> optimizer_applied() const;
+  void consume_optimizer();
+  bool local() const;
 
  private:
   std::shared_ptr<ReducerState> st_;

@@ -422,17 +422,28 @@ __global__ void __launch_bounds__(256) bn_fold_weights_kernel(const uint16_t* __
 // y = W x, dW = sum_m dy^T x = diag(k1) T1 + diag(a) W Gram + b (x) colsum, where T1 = g^T x (the
 // ordinary weight gradient of g), Gram = x^T x and colsum = sum_m x.  out[k][c] (the flat gradient
 // buffer) += that; block 0 also adds dgamma += s1 * invstd, dbeta += s0 (the apply's job before).
-// Blocks: 32x32 tiles of out over (k, c); the K x C x C product W Gram runs through LDS.
-__global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(const float* __restrict__ t1,
-                                                            const float* __restrict__ gram,
+// W is the bf16 mirror the forward used (wt[C][K], the transposed copy bn_fold_weights reads), so
+// the fold's dW matches apply-then-wgrad exactly up to summation order.
+// Blocks: 64x64 tiles of out over (k, c), 4x4 outputs per thread; the K x C x C product W Gram runs
+// through LDS in 32-deep q chunks, two ds_read_b128 per 16 FMAs (the 32x32 / 2x2 version was
+// LDS-issue bound: ~41 us per call in-step, on the weight-gradient stream that ends the step).
+// `done` non-null (consume mode): T1, Gram and the BN-sum accumulator `sums` are persistent
+// workspaces the caller never re-zeroes -- every T1 element is cleared by the thread that reads it;
+// the last block of each 64-column group (counter done[tc]) clears that group's Gram columns; the
+// last group to finish (counter done[nc]) clears sums if `zero_sums` and resets the counters.  No
+// memset or fill launch on the weight-gradient stream.
+constexpr int kFoldTile = 64;
+__global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ t1,
+                                                            float* __restrict__ gram,
                                                             const float* __restrict__ colsum,
-                                                            const float* __restrict__ w, FoldCoef cf, int C,
+                                                            const uint16_t* __restrict__ wt, FoldCoef cf, int C,
                                                             float* __restrict__ out, float* __restrict__ dgamma,
-                                                            float* __restrict__ dbeta) {
+                                                            float* __restrict__ dbeta, int* __restrict__ done,
+                                                            int zero_sums) {
   const int K = cf.K, t = threadIdx.x;
-  const int nc = C / 32;
+  const int nc = C / kFoldTile;
   const int tk = blockIdx.x / nc, tc = blockIdx.x - tk * nc;
-  const int k0 = tk * 32, c0 = tc * 32;
+  const int k0 = tk * kFoldTile, c0 = tc * kFoldTile;
   if (blockIdx.x == 0 && dgamma != nullptr) {
     for (int k = t; k < K; k += 256) {
       const float is = cf.stats[K + k];
@@ -440,51 +451,91 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(const float* __restr
       dbeta[k] += cf.sums[k];
     }
   }
-  __shared__ float sw[32][65], sg[64][33];
-  const int ty = t >> 4, tx = t & 15;  // outputs (k0 + 2ty + i, c0 + 2tx + j)
-  float acc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-  for (int q0 = 0; q0 < C; q0 += 64) {
-    for (int e = t; e < 32 * 64; e += 256) {
-      const int r = e >> 6, q = e & 63;
-      sw[r][q] = w[(size_t)(k0 + r) * C + q0 + q];
+  __shared__ __attribute__((aligned(16))) float sW[32][kFoldTile];  // W^T chunk: [q][k]
+  __shared__ __attribute__((aligned(16))) float sG[32][kFoldTile];  // Gram chunk: [q][c]
+  __shared__ int last;
+  const int ty = t >> 4, tx = t & 15;  // outputs (k0 + 4ty + i, c0 + 4tx + j)
+  float acc[4][4] = {};
+  for (int q0 = 0; q0 < C; q0 += 32) {
+    {  // W: 32 rows q of 64 consecutive k (128 B of bf16): one 16-B load per thread
+      const int q = t >> 3, kk = (t & 7) * 8;
+      f8 v = unpack8(*reinterpret_cast<const uint4*>(wt + (size_t)(q0 + q) * K + k0 + kk));
+      *reinterpret_cast<float4*>(&sW[q][kk]) = make_float4(v.v[0], v.v[1], v.v[2], v.v[3]);
+      *reinterpret_cast<float4*>(&sW[q][kk + 4]) = make_float4(v.v[4], v.v[5], v.v[6], v.v[7]);
     }
-    for (int e = t; e < 64 * 32; e += 256) {
-      const int q = e >> 5, cc = e & 31;
-      sg[q][cc] = gram[(size_t)(q0 + q) * C + c0 + cc];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // Gram: 32 rows q of 64 columns: two float4 per thread
+      const int e = t + h * 256, q = e >> 4, cc = (e & 15) * 4;
+      *reinterpret_cast<float4*>(&sG[q][cc]) = *reinterpret_cast<const float4*>(gram + (size_t)(q0 + q) * C + c0 + cc);
     }
     __syncthreads();
 #pragma unroll 8
-    for (int q = 0; q < 64; ++q) {
-      const float w0 = sw[ty * 2][q], w1 = sw[ty * 2 + 1][q];
-      const float g0 = sg[q][tx * 2], g1 = sg[q][tx * 2 + 1];
-      acc[0][0] = fmaf(w0, g0, acc[0][0]); acc[0][1] = fmaf(w0, g1, acc[0][1]);
-      acc[1][0] = fmaf(w1, g0, acc[1][0]); acc[1][1] = fmaf(w1, g1, acc[1][1]);
+    for (int q = 0; q < 32; ++q) {
+      const float4 w = *reinterpret_cast<const float4*>(&sW[q][ty * 4]);
+      const float4 g = *reinterpret_cast<const float4*>(&sG[q][tx * 4]);
+      const float wv[4] = {w.x, w.y, w.z, w.w}, gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(wv[i], gv[j], acc[i][j]);
     }
     __syncthreads();
   }
+  const float4 cs4 = *reinterpret_cast<const float4*>(colsum + c0 + tx * 4);
+  const float csv[4] = {cs4.x, cs4.y, cs4.z, cs4.w};
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int k = k0 + ty * 2 + i;
+  for (int i = 0; i < 4; ++i) {
+    const int k = k0 + ty * 4 + i;
     const float is = cf.stats[K + k], mu = cf.stats[k];
     const float k1 = cf.gamma[k] * is;
     const float k2 = cf.sums[K + k] * is * is * cf.invM;
     const float a = -k1 * k2, b = -k1 * (cf.sums[k] * cf.invM - mu * k2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = c0 + tx * 2 + j;
-      const size_t o = (size_t)k * C + c;
-      out[o] += k1 * t1[o] + a * acc[i][j] + b * colsum[c];
+    const size_t o = (size_t)k * C + c0 + tx * 4;
+    float4 tv = *reinterpret_cast<const float4*>(t1 + o);
+    float4 ov = *reinterpret_cast<const float4*>(out + o);
+    ov.x += k1 * tv.x + a * acc[i][0] + b * csv[0];
+    ov.y += k1 * tv.y + a * acc[i][1] + b * csv[1];
+    ov.z += k1 * tv.z + a * acc[i][2] + b * csv[2];
+    ov.w += k1 * tv.w + a * acc[i][3] + b * csv[3];
+    *reinterpret_cast<float4*>(out + o) = ov;
+    if (done != nullptr) *reinterpret_cast<float4*>(t1 + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (done == nullptr) return;
+  // every read of gram / sums by this block has returned (their values are consumed above)
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const int nk = K / kFoldTile;
+    int v = atomicAdd(done + tc, 1) == nk - 1 ? 1 : 0;  // last block of column group tc
+    if (v) {
+      done[tc] = 0;
+      __threadfence();
+      v = atomicAdd(done + nc, 1) == nc - 1 ? 2 : 1;    // ... and the last group overall
+      if (v == 2) done[nc] = 0;
     }
+    last = v;
+  }
+  __syncthreads();
+  if (last == 0) return;
+  __threadfence();
+  for (int e = t; e < C * (kFoldTile / 4); e += 256) {  // this group's Gram columns c0 .. c0+63
+    const int q = e >> 4, cc = (e & 15) * 4;
+    *reinterpret_cast<float4*>(gram + (size_t)q * C + c0 + cc) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (last == 2 && zero_sums) {
+    float* sm = const_cast<float*>(cf.sums);
+    for (int e = t; e < 2 * K; e += 256) sm[e] = 0.f;
   }
 }
 
-void launch_bn_fold_wgrad(const float* t1, const float* gram, const float* colsum, const float* w,
+void launch_bn_fold_wgrad(float* t1, float* gram, const float* colsum, const uint16_t* wt,
                           const float* stats, const float* gamma, const float* sums, int M, int C, int K,
-                          float* out, float* dgamma, float* dbeta, hipStream_t st) {
-  if (C % 64 != 0 || K % 32 != 0) throw std::runtime_error("bn_fold_wgrad: needs C % 64 == 0, K % 32 == 0");
+                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st) {
+  if (C % kFoldTile != 0 || K % kFoldTile != 0)
+    throw std::runtime_error("bn_fold_wgrad: needs C % 64 == 0, K % 64 == 0");
   FoldCoef cf{stats, gamma, sums, K, 1.f / (float)M};
-  hipLaunchKernelGGL(bn_fold_wgrad_kernel, dim3((K / 32) * (C / 32)), dim3(256), 0, st, t1, gram, colsum, w, cf, C,
-                     out, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_fold_wgrad_kernel, dim3((K / kFoldTile) * (C / kFoldTile)), dim3(256), 0, st, t1, gram,
+                     colsum, wt, cf, C, out, dgamma, dbeta, done, zero_sums ? 1 : 0);
 }
 
 void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,

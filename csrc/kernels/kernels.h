@@ -126,11 +126,13 @@ struct DgradFold {
 // sums[2][K] (sum g, sum g*(y - mean)) over M rows
 void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
                             int M, int C, int K, uint16_t* wfold, float* bias, hipStream_t st);
-// its weight gradient: out[K][C] += diag(k1) t1 + diag(a) w gram + b colsum^T (t1 = g^T x [K][C],
-// gram = x^T x [C][C], colsum = sum of x [C], w [K][C] fp32); dgamma/dbeta (optional) += s1 * invstd, s0
-void launch_bn_fold_wgrad(const float* t1, const float* gram, const float* colsum, const float* w,
+// its weight gradient: out[K][C] += diag(k1) t1 + diag(a) W gram + b colsum^T (t1 = g^T x [K][C],
+// gram = x^T x [C][C], colsum = sum of x [C], W from the bf16 mirror wt[C][K]); dgamma/dbeta (optional)
+// += s1 * invstd, s0.  done != null: consume mode -- t1, gram (and sums if zero_sums) are cleared for
+// their next use (done: an int completion counter, 0 between launches)
+void launch_bn_fold_wgrad(float* t1, float* gram, const float* colsum, const uint16_t* wt,
                           const float* stats, const float* gamma, const float* sums, int M, int C, int K,
-                          float* out, float* dgamma, float* dbeta, hipStream_t st);
+                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st);
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
                        const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr,
                        int addend_sub = 0, const DgradFold* fold = nullptr);

@@ -10,16 +10,21 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
+#include <stdexcept>
+
 namespace pdt {
 
 // MIRROR: also write bf16(p') to pb -- the KRSC bf16 weights the next forward's convs consume
 // (conv weights are channels_last, so the flat fp32 order already is KRSC), saving a pack pass.
+// `lead` elements before the first 16-B-aligned one (a bucket slice of the flat buffers can start
+// anywhere) and the tail are updated one at a time; the body in float4.  p, g, buf and pb share one
+// element offset from 16-B-aligned bases, so one lead aligns all four.
 template <bool MOM, bool NEST, bool MIRROR>
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ buf, int64_t n, float lr,
                                                   float mom, float damp1, float wd, bool first,
-                                                  float scale, uint16_t* __restrict__ pb) {
-  int64_t n4 = n / 4;
+                                                  float scale, uint16_t* __restrict__ pb, int lead) {
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   auto step = [&](float& pp, float gg, float& bb) {
@@ -30,39 +35,51 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const f
     }
     pp = fmaf(-lr, d, pp);
   };
-  for (int64_t i = tid; i < n4; i += stride) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 bv = MOM ? reinterpret_cast<float4*>(buf)[i] : make_float4(0, 0, 0, 0);
-    step(pv.x, gv.x, bv.x); step(pv.y, gv.y, bv.y); step(pv.z, gv.z, bv.z); step(pv.w, gv.w, bv.w);
-    reinterpret_cast<float4*>(p)[i] = pv;
-    if (MOM) reinterpret_cast<float4*>(buf)[i] = bv;
-    if (MIRROR) reinterpret_cast<uint2*>(pb)[i] = make_uint2(pack2bf(pv.x, pv.y), pack2bf(pv.z, pv.w));
-  }
-  for (int64_t i = n4 * 4 + tid; i < n; i += stride) {
+  auto one = [&](int64_t i) {
     float pv = p[i], bv = MOM ? buf[i] : 0.f;
     step(pv, g[i], bv);
     p[i] = pv;
     if (MOM) buf[i] = bv;
     if (MIRROR) pb[i] = f2bf(pv);
+  };
+  if (tid < lead) one(tid);
+  const int64_t n4 = (n - lead) / 4;
+  float4* p4 = reinterpret_cast<float4*>(p + lead);
+  const float4* g4 = reinterpret_cast<const float4*>(g + lead);
+  float4* b4 = reinterpret_cast<float4*>(buf + lead);
+  uint2* pb4 = reinterpret_cast<uint2*>(pb + lead);
+  for (int64_t i = tid; i < n4; i += stride) {
+    float4 pv = p4[i];
+    float4 gv = g4[i];
+    float4 bv = MOM ? b4[i] : make_float4(0, 0, 0, 0);
+    step(pv.x, gv.x, bv.x); step(pv.y, gv.y, bv.y); step(pv.z, gv.z, bv.z); step(pv.w, gv.w, bv.w);
+    p4[i] = pv;
+    if (MOM) b4[i] = bv;
+    if (MIRROR) pb4[i] = make_uint2(pack2bf(pv.x, pv.y), pack2bf(pv.z, pv.w));
   }
+  for (int64_t i = lead + n4 * 4 + tid; i < n; i += stride) one(i);
 }
 
 template <bool MIRROR>
 static void launch_sgd_t(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,
                          float dampening, float wd, bool nesterov, bool first, float grad_scale,
                          hipStream_t st, uint16_t* pb) {
+  if (n <= 0) return;
+  const int lead = (int)std::min<int64_t>(n, (int64_t)(((16 - ((uintptr_t)p & 15)) & 15) >> 2));
+  if (((uintptr_t)g & 15) != ((uintptr_t)p & 15) || (buf && ((uintptr_t)buf & 15) != ((uintptr_t)p & 15)) ||
+      (pb && ((uintptr_t)(pb + lead) & 7) != 0) || ((uintptr_t)p & 3))
+    throw std::runtime_error("sgd: flat buffers must share their 16-byte alignment");
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 4096) blocks = 4096;
   dim3 gr((unsigned)blocks), bl(256);
   float damp1 = 1.f - dampening;
   if (momentum == 0.f)
-    hipLaunchKernelGGL((sgd_kernel<false, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
+    hipLaunchKernelGGL((sgd_kernel<false, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb, lead);
   else if (nesterov)
-    hipLaunchKernelGGL((sgd_kernel<true, true, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
+    hipLaunchKernelGGL((sgd_kernel<true, true, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb, lead);
   else
-    hipLaunchKernelGGL((sgd_kernel<true, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb);
+    hipLaunchKernelGGL((sgd_kernel<true, false, MIRROR>), gr, bl, 0, st, p, g, buf, n, lr, momentum, damp1, wd, first, grad_scale, pb, lead);
 }
 
 void launch_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum,

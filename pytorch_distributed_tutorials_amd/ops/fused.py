@@ -1151,16 +1151,18 @@ class _ResidualBlock(torch.autograd.Function):
                 fold = C.bn_fold_weights(wt.view(c_, k_), stt, gamma, sums, count)
                 # the weight gradient without dy either: dW = diag(k1) g^T x + diag(a) W x^T x + b sum(x),
                 # on the side stream (also the BN parameter gradients and the accumulator re-zero)
-                streams.fork(side, g, stt, sums, xin)
+                streams.fork(side, g, stt, sums, wt, xin)
                 with torch.cuda.stream(side):
-                    t1 = C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, False)
-                    gram = C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, False)
+                    # T1 and Gram accumulate into persistent zeroed workspaces that bn_fold_wgrad
+                    # clears after reading (with the consumed BN-sum accumulator): no memset / fill
+                    t1, gram, done = _fold_ws(k_, c_, xin.device)
+                    C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, False, t1)
+                    C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, False, gram)
                     colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
                     dfr = deferred.pop(5 * i, None)
-                    C.bn_fold_wgrad(t1, gram, colsum, w, stt, gamma, sums, count, _grad_sink(params[5 * i]),
-                                    dfr[1] if dfr is not None else None, dfr[2] if dfr is not None else None)
-                    if dfr is not None:
-                        dfr[0].zero_()
+                    C.bn_fold_wgrad(t1, gram, colsum, wt.view(c_, k_), stt, gamma, sums, count,
+                                    _grad_sink(params[5 * i]), dfr[1] if dfr is not None else None,
+                                    dfr[2] if dfr is not None else None, done, dfr is not None)
                 sunk.append(params[5 * i])
             elif pre is not None:
                 dy, _, d8 = apply(5 * i, g, g, y, stt, sums, 0, tr, False, need_dx, in8[i] if in8 else None, st)
@@ -1250,6 +1252,18 @@ def _fold_ok(i, last, w, xin, st, pd, tr, det, side, fp8b, params) -> bool:
 
 
 _ZSTATS = {}
+_FOLD_WS = {}
+
+
+def _fold_ws(k, c, dev):
+    """Persistent (T1 [k, c, 1, 1], Gram [c, c, 1, 1], completion counter) fp32 workspaces of the
+    folded weight gradient, zeroed once; every consumer (bn_fold_wgrad in consume mode) leaves them
+    zeroed again.  Units of one shape reuse them in order on the weight-gradient stream."""
+    ws = _FOLD_WS.get((k, c, dev))
+    if ws is None:
+        ws = _FOLD_WS[(k, c, dev)] = (torch.zeros(k, c, 1, 1, device=dev), torch.zeros(c, c, 1, 1, device=dev),
+                                      torch.zeros(c // 64 + 1, dtype=torch.int32, device=dev))
+    return ws
 
 
 def _zero_stats(c, dev):

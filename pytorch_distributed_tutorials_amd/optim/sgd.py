@@ -11,6 +11,17 @@ HIP kernel over the flat param/grad/momentum buffers (``csrc/kernels/sgd.hip``).
 The per-parameter ``state[p]['momentum_buffer']`` entries are views into the
 flat momentum buffer, so ``state_dict()`` / ``load_state_dict()`` keep torch's
 format.  Anything else falls back to a per-tensor reference implementation.
+
+Optimizer in backward (``overlap``, default: wherever it applies).  When the flat space belongs to
+our ``DistributedDataParallel`` on a GPU, the update is launched per gradient bucket INSIDE
+backward, right behind that bucket's all-reduce (or, in one process, as soon as the bucket's
+gradients are final), so only the last bucket's update follows backward; ``step()`` then only
+joins.  The math is the same kernel over the same elements, so parameters are bitwise equal to the
+post-backward step (``tests/test_opt_overlap_gpu.py``).  Contract, checked loudly: every synced
+backward is followed by ``step()`` before the next forward, and neither the gradients nor the
+hyperparameters change in between (gradient clipping, an LR change between backward and step):
+``SGD(..., overlap=False)`` keeps the classic post-backward step for such loops.  ``no_sync()``
+backwards are not updated (their gradients accumulate as usual).
 """
 from __future__ import annotations
 
@@ -22,7 +33,7 @@ from ..ops._ext import native
 
 class SGD(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
-                 weight_decay: float = 0.0, nesterov: bool = False):
+                 weight_decay: float = 0.0, nesterov: bool = False, overlap=None):
         if lr < 0.0:
             raise ValueError(f"Invalid learning rate: {lr}")
         if nesterov and (momentum <= 0 or dampening != 0):
@@ -31,6 +42,56 @@ class SGD(torch.optim.Optimizer):
                         weight_decay=weight_decay, nesterov=nesterov)
         super().__init__(params, defaults)
         self._flat_bufs = {}
+        self._flat_first = {}   # flat space id -> the next update initialises the momentum buffer
+        self._armed = None      # hyperparameters the reducer's per-bucket update was armed with
+        self._overlap_owner = None
+        if overlap is not False:
+            self._attach_overlap()
+
+    # ------------------------------------------------------------ optimizer in backward
+    def _attach_overlap(self) -> None:
+        if len(self.param_groups) != 1:
+            return
+        sp = self._flat_space_of(self.param_groups[0])
+        owner = getattr(sp, "owner", None) if sp is not None else None
+        ddp = owner() if owner is not None else None
+        if ddp is not None and sp.param_flat.is_cuda and ddp.attach_optimizer(self):
+            self._overlap_owner = owner
+
+    def _flat_momentum(self, sp, mom):
+        """(flat momentum buffer or None, is this the buffer's first update?)"""
+        key = id(sp)
+        if mom != 0 and key not in self._flat_bufs:
+            buf = torch.empty_like(sp.param_flat)
+            self._flat_bufs[key] = buf
+            for p, o in zip(sp.params, sp.offsets):
+                self.state[p]["momentum_buffer"] = torch.as_strided(buf, p.shape, p.stride(), o)
+            self._flat_first[key] = not self._restored_momentum(sp)
+        return self._flat_bufs.get(key), self._flat_first.get(key, False)
+
+    def _hyper(self, group):
+        return (group["lr"], group["momentum"], group["dampening"], group["weight_decay"], group["nesterov"])
+
+    def _arm_overlap(self, reducer) -> None:
+        """Called by the DDP wrapper's forward before a synced backward: arm the per-bucket update."""
+        if self._armed is not None and reducer.optimizer_applied()[0] >= 0:
+            raise RuntimeError(
+                "optimizer overlap: a backward already applied this optimizer's update per bucket, but "
+                "step() was not called before the next forward.  Call optimizer.step() after every "
+                "synced backward, or construct the optimizer with overlap=False")
+        self._armed = None
+        if torch.cuda.is_current_stream_capturing():
+            return  # a captured step keeps the post-backward update (utils/graph.py)
+        group = self.param_groups[0]
+        sp = self._flat_space_of(group)
+        if sp is None:
+            return
+        hp = self._hyper(group)
+        lr, mom, damp, wd, nest = hp
+        buf, first = self._flat_momentum(sp, mom)
+        mirror = sp.mirror()
+        reducer.arm_optimizer(lr, mom, damp, wd, nest, first, buf, mirror.krsc if mirror is not None else None)
+        self._armed = hp
 
     def _flat_space_of(self, group):
         ps = group["params"]
@@ -78,20 +139,19 @@ class SGD(torch.optim.Optimizer):
             wd, nest = group["weight_decay"], group["nesterov"]
             sp = self._flat_space_of(group)
             if sp is not None and sp.param_flat.is_cuda:
+                mirror = sp.mirror()
+                if self._armed is not None and self._overlap_step(sp, group):
+                    # every bucket was updated inside backward (and the caller's stream joined it)
+                    self._flat_first[id(sp)] = False
+                    if mirror is not None:
+                        mirror.after_optimizer_step()
+                    continue
                 if not sp.grads_attached():
                     sp.gather_grads()
-                key = id(sp)
-                first = False
-                if mom != 0 and key not in self._flat_bufs:
-                    buf = torch.empty_like(sp.param_flat)
-                    self._flat_bufs[key] = buf
-                    for p, o in zip(sp.params, sp.offsets):
-                        self.state[p]["momentum_buffer"] = torch.as_strided(buf, p.shape, p.stride(), o)
-                    first = not self._restored_momentum(sp)
-                buf = self._flat_bufs.get(key)
-                mirror = sp.mirror()
+                buf, first = self._flat_momentum(sp, mom)
                 native().sgd_step(sp.param_flat, sp.grad_flat, buf, lr, mom, damp, wd, nest,
                                   first, 1.0, mirror.krsc if mirror is not None else None)
+                self._flat_first[id(sp)] = False
                 if mirror is not None:
                     mirror.after_optimizer_step()  # bf16 conv weights for the next forward
                 continue
@@ -111,6 +171,26 @@ class SGD(torch.optim.Optimizer):
                 ref.sgd_momentum_(
                     [p], [g], [b], lr, mom, damp, wd, nest, f)
         return loss
+
+    def _overlap_step(self, sp, group) -> bool:
+        """True if the last backward applied this step per bucket; validates the contract."""
+        owner = self._overlap_owner() if self._overlap_owner is not None else None
+        armed, self._armed = self._armed, None
+        if owner is None or owner.reducer is None:
+            return False
+        applied, gver = owner.reducer.optimizer_applied()
+        if applied < 0:
+            return False  # armed, but no synced backward ran (e.g. a forward without backward)
+        owner.reducer.consume_optimizer()
+        if applied != owner.reducer.num_buckets:
+            raise RuntimeError(f"optimizer overlap: {applied} of {owner.reducer.num_buckets} buckets updated")
+        if self._hyper(group) != armed:
+            raise RuntimeError("optimizer overlap: hyperparameters changed between backward and step() "
+                               "(the update already ran in backward); use SGD(..., overlap=False)")
+        if sp.grad_flat._version != gver or not sp.grads_attached():
+            raise RuntimeError("optimizer overlap: gradients were modified between backward and step() "
+                               "(the update already ran in backward); use SGD(..., overlap=False)")
+        return True
 
     def _restored_momentum(self, sp) -> bool:
         """True if load_state_dict() populated momentum buffers before the first step."""

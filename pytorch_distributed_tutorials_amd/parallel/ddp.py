@@ -30,6 +30,7 @@ from __future__ import annotations
 import contextlib
 import os
 import warnings
+import weakref
 from typing import List, Optional
 
 import torch
@@ -210,6 +211,9 @@ class DistributedDataParallel(nn.Module):
                                   exit_on_error=self.comm_options.exit_on_error)
             grad_storage = self.xgmi.grad_buffer()
         self.space = FlatParamSpace([params[i] for i in layout], grad_flat=grad_storage)
+        self.space.owner = weakref.ref(self)  # optim.SGD finds the wrapper (attach_optimizer) here
+        self._opt_overlap = None  # weakref to the optimizer whose update runs per bucket in backward
+        self._bucket_of = [bi for bi, b in enumerate(plan) for _ in b]
         self.bucket_ranges = []
         pos = 0
         for b in plan:
@@ -351,10 +355,47 @@ class DistributedDataParallel(nn.Module):
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self.require_forward_param_sync = True
             if self.reducer is not None:
+                opt = self._opt_overlap() if self._opt_overlap is not None else None
+                if opt is not None:
+                    opt._arm_overlap(self.reducer)
                 self.reducer.prepare_for_backward()
         else:
             self.require_forward_param_sync = False
         return out
+
+    def attach_optimizer(self, opt) -> bool:
+        """Run ``opt``'s update (our fused SGD) per bucket inside backward, right behind each
+        bucket's all-reduce on the comm stream -- or, in one process, on the reducer's local stream
+        as soon as the bucket's gradients are final -- so that only the last bucket's update is left
+        after backward.  ``opt.step()`` then only joins.  Needs the native
+        extension, a GPU and a native communicator (or one process: the reducer is then created in
+        local mode).  Returns False where it does not apply (the optimizer then steps as usual)."""
+        if self.device.type != "cuda" or not native_available():
+            return False
+        if self.reducer is None:
+            if self.world_size > 1:
+                return False
+            from ..ops._ext import native
+            sp = self.space
+            flats = [sp.grad_flat.narrow(0, s, e - s) for s, e in self.bucket_ranges]
+            # local mode: no communicator, no Python launch -- the optimizer-overlap stream only
+            self.reducer = native().Reducer(sp.params, sp.grad_views, self._bucket_of, flats, None, None, None,
+                                            self.average, "fp32", xgmi=None)
+            self._flats = flats
+            sp.reducer = self.reducer
+            from ..ops import streams
+            side = streams.wgrad_stream(self.device)
+            if side is not None:
+                self.reducer.set_aux_stream(side.cuda_stream)
+        elif (self.comm is None and self.xgmi is None and not getattr(self.reducer, "local", False)) \
+                or not hasattr(self.reducer, "arm_optimizer") or self.wire_dtype != "fp32":
+            return False  # gradients through torch.distributed (gloo) or the bf16 wire: step() as usual
+        self.reducer.set_optimizer(self.space.param_flat, self.space.grad_flat)
+        self._opt_overlap = weakref.ref(opt)
+        return True
+
+    def detach_optimizer(self) -> None:
+        self._opt_overlap = None
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -368,7 +409,8 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------- metrics
     def enable_comm_timing(self, on: bool = True) -> bool:
         """Record HIP events around each iteration's all-reduces (native RCCL / xGMI paths)."""
-        if self.reducer is None or (self.comm is None and self.xgmi is None) \
+        if self.reducer is None or (self.comm is None and self.xgmi is None
+                                    and not getattr(self.reducer, "local", False)) \
                 or not hasattr(self.reducer, "set_timing"):
             return False
         self.reducer.set_timing(on)

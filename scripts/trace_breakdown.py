@@ -1,14 +1,20 @@
 """Per-step kernel time by stream and kernel family from a rocprofv3 kernel trace (the last full
-step between two optimizer launches): python scripts/trace_breakdown.py run_kernel_trace.csv"""
+step between two launches of the marker kernel -- the stem's image conversion, the first kernel of a
+step; the per-bucket optimizer launches several SGD kernels per step):
+python scripts/trace_breakdown.py run_kernel_trace.csv [marker]"""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
-a, b = idx[-2], idx[-1]
-step = rows[a + 1:b + 1]
+marker = sys.argv[2] if len(sys.argv) > 2 else "stem_image_kernel"
+idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+# the last marker pair whose span is not an outlier (the bench's checksum / diagnostic steps follow)
+spans = [(int(rows[j]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]), i, j) for i, j in zip(idx, idx[1:])]
+med = sorted(sp for sp, _, _ in spans)[len(spans) // 2]
+a, b = [(i, j) for sp, i, j in spans if sp < 1.5 * med][-1]
+step = rows[a:b]
 t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
 print(f"step span {(t1 - t0) / 1000:.1f} us, {len(step)} kernels")
 

@@ -31,15 +31,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=15)
-    ap.add_argument("--step-marker", default="sgd_kernel",
-                    help="kernel that ends a training step; only the last complete step is analysed")
+    ap.add_argument("--step-marker", default="stem_image_kernel",
+                    help="kernel that starts a training step; the last complete step of typical length "
+                         "(the bench's diagnostic steps that follow are skipped) is analysed")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if a.step_marker and a.step_marker in r["Kernel_Name"]]
-    if len(ends) >= 2:  # the last complete step: after the previous marker up to the last one
-        rows = rows[ends[-2] + 1:ends[-1] + 1]
-        print(f"last step only ({len(rows)} kernels, marker {a.step_marker})")
+    idx = [i for i, r in enumerate(rows) if a.step_marker and a.step_marker in r["Kernel_Name"]]
+    if len(idx) >= 2:
+        spans = [(int(rows[j]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]), i, j)
+                 for i, j in zip(idx, idx[1:])]
+        med = sorted(sp for sp, _, _ in spans)[len(spans) // 2]
+        i0, i1 = [(i, j) for sp, i, j in spans if sp < 1.5 * med][-1]
+        rows = rows[i0:i1]
+        print(f"last typical step only ({len(rows)} kernels, marker {a.step_marker})")
     iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:90]) for r in rows]
     by_q = defaultdict(list)
     for r, x in zip(rows, iv):
