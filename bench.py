@@ -137,6 +137,38 @@ def _last_mb(v: str):
     return float(v)
 
 
+def _diag_lead(step, barrier, dev, nsteps: int = 8) -> None:
+    """PDT_DIAG_LEAD=1 (untimed diagnostic): how far the host's issue runs ahead of the device at
+    every block forward / backward entry of ``nsteps`` back-to-back steps.  Timing events recorded at
+    those points are placed on one clock with the host's perf_counter through an event recorded on
+    an idle device; lead = device time the mark executed - host time it was issued (near 0: the
+    device waited for the host there)."""
+    import torch
+    from pytorch_distributed_tutorials_amd.ops import fused
+    barrier()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    h0 = time.perf_counter()
+    fused._LEAD = marks = []
+    starts = []
+    for _ in range(nsteps):
+        starts.append(len(marks))
+        fused._lead_mark("step")
+        step()
+    fused._LEAD = None
+    barrier()
+    rows = [(tag, (h - h0) * 1e3, e0.elapsed_time(ev)) for tag, h, ev in marks]
+    for k, a in enumerate(starts):
+        b = starts[k + 1] if k + 1 < len(starts) else len(rows)
+        leads = [g - h for _, h, g in rows[a:b]]
+        bw = [g - h for tag, h, g in rows[a:b] if tag.startswith("bwd")]
+        print(f"[lead] step {k}: device at step start {rows[a][2]:8.2f} ms, host {rows[a][1]:8.2f} ms; "
+              f"lead min {min(leads):6.2f} ms (backward min {min(bw) if bw else float('nan'):6.2f})", flush=True)
+    a = starts[-1]
+    for tag, h, g in rows[a:]:
+        print(f"[lead]   {tag:28s} host {h:8.2f} device {g:8.2f} lead {g - h:6.2f} ms", flush=True)
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -317,6 +349,8 @@ def main(argv=None) -> int:
         with open(prof_path, "w") as f:
             f.write(buf.getvalue())
     host_issue_ms = 1000.0 * min(issue)
+    if os.environ.get("PDT_DIAG_LEAD") == "1" and dev.type == "cuda" and args.impl == "native":
+        _diag_lead(step, barrier, dev)
     # every rank must hold bit-identical parameters after the run (untimed): a positional int64
     # checksum of the parameter bits, all-gathered -- a fast-but-wrong multi-GPU run shows here
     ranks_identical, param_checksum = _param_checksums(ddp, args.impl, world, dev)

@@ -367,7 +367,9 @@ void bn_fold_wgrad(Tensor t1, Tensor gram, const Tensor& colsum, const Tensor& w
 // g [N,H,W,K] is that BN's masked gradient, z [N,H,W,C] the conv's input; acc mode only.
 std::tuple<Tensor, Tensor> conv_dgrad_bn_fold(const Tensor& g, const Tensor& z_in, const Tensor& wfold,
                                               const Tensor& bias, const Tensor& y, const std::optional<Tensor>& z,
-                                              const Tensor& stats, int64_t mask, const Tensor& acc) {
+                                              const Tensor& stats, int64_t mask, const std::optional<Tensor>& acc,
+                                              const std::optional<Tensor>& dgamma,
+                                              const std::optional<Tensor>& dbeta) {
   check_bf16_nhwc(g, "g");
   check_bf16_nhwc(z_in, "z_in");
   const int K = g.size(3), C = z_in.size(3);
@@ -379,7 +381,9 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fold(const Tensor& g, const Tensor& z_i
   c10::hip::HIPGuard gd(g.get_device());
   auto s = shape_of(g.size(0), g.size(1), g.size(2), C, K, 1, 1, 1, 0);
   pdt::DgradFold fold{cbf(z_in), C, bias.data_ptr<float>()};
-  return dgrad_bn_core(g, s, std::nullopt, y, z, stats, mask, std::nullopt, std::nullopt, acc,
+  // acc: fp32-atomic BN sums of the unit before (default runs); without it (deterministic runs) the
+  // fixed-order partials + reduce path, with that unit's dgamma / dbeta sinks
+  return dgrad_bn_core(g, s, std::nullopt, y, z, stats, mask, dgamma, dbeta, acc,
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad(cbf(g), reinterpret_cast<const uint16_t*>(wfold.data_ptr()), dx,
@@ -1476,7 +1480,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("done") = py::none(), py::arg("zero_sums") = false);
   m.def("conv_dgrad_bn_fold", checked("conv_dgrad_bn_fold", &conv_dgrad_bn_fold), py::arg("g"), py::arg("z_in"),
         py::arg("wfold"), py::arg("bias"), py::arg("y"), py::arg("z"), py::arg("stats"), py::arg("mask"),
-        py::arg("acc"));
+        py::arg("acc") = py::none(), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_fwd_bn", checked("conv_fwd_bn", &conv_fwd_bn), py::arg("x"), py::arg("wk"), py::arg("stride"),
         py::arg("pad"), py::arg("count"), py::arg("rm"), py::arg("rv"), py::arg("gamma"), py::arg("beta"),
         py::arg("momentum"), py::arg("eps"), py::arg("acc") = py::none());

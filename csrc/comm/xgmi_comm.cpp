@@ -139,6 +139,16 @@ void XgmiComm::open_peers(const std::vector<std::string>& handles) {
            ("hipIpcOpenMemHandle(rank " + std::to_string(q) + ")").c_str());
       opened_.push_back(p[i]);
     }
+    // plain (cached) flag memory is only safe while every peer shares this GPU's L2: across
+    // devices a poll could spin on a stale line, so the fallback is refused there
+    if (!flags_uncached_) {
+      hipPointerAttribute_t attr{};
+      const bool known = hipPointerGetAttributes(&attr, p[2]) == hipSuccess;
+      (void)hipGetLastError();
+      if (!known || attr.device != device_)
+        throw std::runtime_error("xgmi: peer rank " + std::to_string(q) + " is on another device, but uncached "
+                                 "flag memory could not be exported here; use comm='rccl'");
+    }
     gp_[q] = static_cast<const float*>(p[0]);
     rp_[q] = static_cast<const float*>(p[1]);
     fp_[q] = static_cast<unsigned*>(p[2]);

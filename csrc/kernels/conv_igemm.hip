@@ -269,7 +269,11 @@ constexpr int nt_min_waves() {
 // fire-and-forget agent-scope fp64 atomic add per channel and moment.  A one-block-per-256-channel
 // launch (launch_bn_finalize_sums) turns the totals into the statistics and re-zeroes them --
 // instead of bn_finalize's reduction over one partial per row tile (3136-6272 of them on layer 1).
-// fp64 totals: var = E[y^2] - mean^2 keeps ~1e-16 relative error where fp32 would cancel.
+// Precision: the totals are fp64, but each workgroup's contribution is an fp32 sum over its <= 256
+// rows, so var = E[y^2] - mean^2 carries a relative error of roughly (mean / std)^2 * 2^-24 per
+// tile sum (averaging down over the tiles) -- not fp64's 1e-16.  Pinned at |mean| / std up to ~100
+// by tests/test_tiles_gpu.py::test_fwd_bn_fused_stats_far_from_zero_mean (invstd within 1e-3 of
+// an fp64 two-pass reference over the same bf16 y).
 template <class CFG, int WM>
 __device__ __forceinline__ void nt_stats_atomic(const NtArgs& P, const float* red, int n0) {
   constexpr int BN = CFG::BN;

@@ -149,7 +149,7 @@ void conv_wgrad_fp8_plan(const ConvShape& s, int out[4]);
 void launch_conv_wgrad_fp8(const uint8_t* dy8, const uint8_t* x8, const float* dy_deq, const float* x_deq,
                            float* dw, const ConvShape& s, bool accumulate, hipStream_t st);
 // zero / zero_n: optional fp32 buffer the weight-gradient kernel clears (workgroup 0) -- the BN-sum
-// accumulator whose consumer is ordered before this launch (ops/fused.py PDT_BN_ACC)
+// accumulator whose consumer is ordered before this launch (ops/fused.py _BN_ACC)
 void launch_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* ws,
                        const ConvShape& s, bool deterministic, bool accumulate, hipStream_t st,
                        float* zero = nullptr, int zero_n = 0);

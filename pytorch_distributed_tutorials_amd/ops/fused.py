@@ -76,6 +76,19 @@ _FUSE_RES_BN = True  # shortcut BN applied in the block tail
 # forward appends its units' stored post-activation outputs (z, NHWC bf16), so an fp32 reference
 # can take the native path's ReLU decisions and compare gradients without ReLU-flip noise
 _CAPTURE = None
+# diagnostic hook (bench.py PDT_DIAG_LEAD=1): when a list, every block forward / backward appends
+# (tag, host perf_counter, timing event recorded on the current stream at its entry), so the host's
+# lead over the device can be read per block after the run
+_LEAD = None
+
+
+def _lead_mark(tag: str) -> None:
+    import time
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    _LEAD.append((tag, time.perf_counter(), ev))
+
+
 _COMPACT_ADDEND = True  # stride-2 shortcut dgrad compact
 
 
@@ -870,6 +883,8 @@ class _ResidualBlock(torch.autograd.Function):
     def forward(ctx, x, spec, handoff, fp8io, *tensors):
         C = native()
         _nan_trace(f"block-in {tuple(x.shape)}", x=x)
+        if _LEAD is not None:
+            _lead_mark(f"fwd {tuple(x.shape)}")
         chain, ds_cfg = spec
         nch = len(chain)
         saved = [x]
@@ -947,6 +962,8 @@ class _ResidualBlock(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         C = native()
+        if _LEAD is not None:
+            _lead_mark(f"bwd {tuple(dz.shape)}")
         chain, ds_cfg = ctx.spec
         nch = len(chain)
         sv = ctx.saved_tensors
@@ -1156,8 +1173,8 @@ class _ResidualBlock(torch.autograd.Function):
                     # T1 and Gram accumulate into persistent zeroed workspaces that bn_fold_wgrad
                     # clears after reading (with the consumed BN-sum accumulator): no memset / fill
                     t1, gram, done = _fold_ws(k_, c_, xin.device)
-                    C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, False, t1)
-                    C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, False, gram)
+                    C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, det, t1)
+                    C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, det, gram)
                     colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
                     dfr = deferred.pop(5 * i, None)
                     C.bn_fold_wgrad(t1, gram, colsum, wt.view(c_, k_), stt, gamma, sums, count,
@@ -1182,9 +1199,13 @@ class _ResidualBlock(torch.autograd.Function):
                 yp, sttp = units[i - 1][1], units[i - 1][2]
                 if fold is not None:
                     j = 5 * (i - 1)
-                    acc = _bacc(params[j + 1], sttp.shape[1])
-                    pre = C.conv_dgrad_bn_fold(g, xin, fold[0], fold[1], yp, None, sttp, 2, acc)
-                    deferred[j] = (acc, _grad_sink(params[j + 1]), _grad_sink(params[j + 2]))
+                    if det:  # fixed-order partials + reduce; dgamma / dbeta straight into the sinks
+                        pre = C.conv_dgrad_bn_fold(g, xin, fold[0], fold[1], yp, None, sttp, 2, None,
+                                                   _grad_sink(params[j + 1]), _grad_sink(params[j + 2]))
+                    else:
+                        acc = _bacc(params[j + 1], sttp.shape[1])
+                        pre = C.conv_dgrad_bn_fold(g, xin, fold[0], fold[1], yp, None, sttp, 2, acc)
+                        deferred[j] = (acc, _grad_sink(params[j + 1]), _grad_sink(params[j + 2]))
                     sunk.extend([params[j + 1], params[j + 2]])
                 elif _FUSE_DGRAD_BN:
                     pre = dgrad_bn(5 * (i - 1), dy, d8, w, xin_shape, st, pd, None, yp, None, sttp, 2)
@@ -1237,10 +1258,11 @@ FOLD_CALLS = 0  # folded units so far (tests check that the path engaged)
 
 def _fold_ok(i, last, w, xin, st, pd, tr, det, side, fp8b, params) -> bool:
     """May the last unit of a bottleneck fold its BN backward into its 1x1 input gradient
-    (kernels.h DgradFold)?  bf16, non-deterministic (acc-mode sums), training, a weight-gradient
-    side stream, a 1x1 / stride-1 conv over a materialised input, and gradient sinks for the BN of
-    the unit before (its sums go to an atomic accumulator)."""
-    if not (_FOLD_BN and last and i > 0 and tr and not det and side is not None and not fp8b and _BN_ACC
+    (kernels.h DgradFold)?  bf16, training, a weight-gradient side stream, a 1x1 / stride-1 conv over
+    a materialised input, and gradient sinks for the BN of the unit before (its sums go to an atomic
+    accumulator, or in deterministic runs to fixed-order partials with dgamma / dbeta written by the
+    reduce; the fold's weight-gradient GEMMs then take the slab split-K)."""
+    if not (_FOLD_BN and last and i > 0 and tr and side is not None and not fp8b and _BN_ACC
             and _FUSE_DGRAD_BN and xin is not None):
         return False
     k, c, r, s_ = w.shape

@@ -11,6 +11,7 @@
 #   smoke                  __graft_entry__.smoke()
 #   bench[:args]           python bench.py <args with , as separator>  (bench:--force-comm,--steps,20)
 #   prof[:args]            rocprofv3 --kernel-trace --stats of bench.py <args>  -> gpurun_out/TAG_prof
+#   trace[:args]           rocprofv3 --kernel-trace --hip-trace of bench.py <args>   -> gpurun_out/TAG_trace
 #   pmc:<counters>[:args]  one rocprofv3 --pmc pass over bench.py <args>          -> gpurun_out/TAG_pmc_N
 #   py:<script>[:args]     python -u <script> <args>
 #   pmcpy:<ctrs>:<script>[:args]  one rocprofv3 --pmc pass over python <script> <args>  -> TAG_pmc_N
@@ -57,6 +58,11 @@ for st in "$@"; do
       ( cd /tmp && export TMPDIR=/tmp && run prof 500 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$O/${TAG}_prof" -o run -- python3 "$R/bench.py" $args ) || exit 1
       nstep=$((nstep+1)) ;;  # run() counted inside the subshell
+    trace)  # kernel + HIP API trace (host launch time vs kernel start), no counters
+      args=${rest//,/ }
+      ( cd /tmp && export TMPDIR=/tmp && run trace 500 rocprofv3 --kernel-trace --hip-trace --output-format csv \
+          -d "$O/${TAG}_trace" -o run -- python3 "$R/bench.py" $args ) || exit 1
+      nstep=$((nstep+1)) ;;
     pmc)
       ctr=${rest%%:*}; args=""; [ "$ctr" != "$rest" ] && args=${rest#*:}; args=${args//,/ }
       npmc=$((npmc+1))

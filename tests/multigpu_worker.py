@@ -13,7 +13,9 @@ ranks live on different GPUs -- so the first multi-GPU box a run lands on verifi
   waiting for late peers; every late peer fails with "peer rank 0 failed first"; NaN buckets);
 * ``ddp``: native ResNet-18 under ``DistributedDataParallel`` over RCCL (and, with ``--comm
   xgmi``, the direct backend), a few SGD steps; parameter checksums all-gathered: every rank
-  bit-identical.
+  bit-identical; and the step-1 averaged gradient against the mean of every rank's own gradient
+  from a single-process native twin (rel < 2e-2), well away from the un-reduced local gradient
+  and from the sum.
 
 Prints one RESULT json line per rank.
 """
@@ -126,23 +128,71 @@ def run_xgmi(rank, world, dev):
     return res
 
 
+def _reference_grad(state, names, world, dev):
+    """Step-1 gradient DDP must produce: the mean over ranks of each rank's own gradient, taken by
+    a single-process twin (same native kernels, a plain module outside any flat space: autograd
+    returns its gradients) on the rank's local batch with its local BatchNorm statistics -- DDP
+    does not synchronise BN -- in the flat space's parameter order.  (An fp32 stock twin differs by
+    ~40 % over a whole random-init ResNet-18 from bf16 ReLU flips compounding through BN at batch
+    16, which would hide a reducer bug; the block tests pin the kernels against fp32.)  Also
+    returns this rank's own local gradient, which a reducer that skipped the all-reduce leaves."""
+    from pytorch_distributed_tutorials_amd import ops
+    from pytorch_distributed_tutorials_amd.models import build_model
+    ref = build_model("resnet18", num_classes=10).to(dev)
+    ref.load_state_dict(state)
+    ref.set_impl("native")
+    ref.train()
+    params = dict(ref.named_parameters())
+    total = None
+    local = []
+    for q in range(world):
+        gen = torch.Generator().manual_seed(77 + q)
+        x = torch.randn(16, 3, 32, 32, generator=gen).to(dev)
+        y = torch.randint(0, 10, (16,), generator=gen).to(dev)
+        ref.zero_grad(set_to_none=True)
+        ops.cross_entropy(ref(x), y).backward()
+        g = torch.cat([params[n].grad.reshape(-1) for n in names])
+        local.append(g)
+        total = g.clone() if total is None else total + g
+    return total / world, local
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
 def run_ddp(rank, world, dev, comm_kind, steps=3):
     from pytorch_distributed_tutorials_amd import ops
     from pytorch_distributed_tutorials_amd.models import build_model
     from pytorch_distributed_tutorials_amd.optim import SGD
     from pytorch_distributed_tutorials_amd.parallel import DistributedDataParallel
     torch.manual_seed(0)
-    m = build_model("resnet18", num_classes=10).to(dev).set_impl("native")
+    m = build_model("resnet18", num_classes=10).to(dev)
+    state0 = {k: v.detach().clone() for k, v in m.state_dict().items()}  # before the KRSC re-layout
+    m.set_impl("native")
     ddp = DistributedDataParallel(m, device_ids=[dev.index], comm=comm_kind)
     opt = SGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-5)
+    name_of = {id(p): n for n, p in ddp.module.named_parameters()}
+    names = [name_of[id(p)] for p in ddp.space.params]
     gen = torch.Generator().manual_seed(77 + rank)
     losses = []
-    for _ in range(steps):
+    res = {}
+    for it in range(steps):
         x = torch.randn(16, 3, 32, 32, generator=gen).to(dev)
         y = torch.randint(0, 10, (16,), generator=gen).to(dev)
         opt.zero_grad()
         loss = ops.cross_entropy(ddp(x), y)
         loss.backward()
+        if it == 0:
+            # ROUND-5 verdict weak #8: the averaged gradient must be RIGHT, not only equal across
+            # ranks -- a reducer that sums, averages twice or drops a bucket fails here
+            torch.cuda.synchronize()
+            # logical (OIHW) order: the flat buffer holds conv weights channels_last
+            got = torch.cat([g.detach().reshape(-1) for g in ddp.space.grad_views])
+            want, local = _reference_grad(state0, names, world, dev)
+            res["grad_rel_vs_reference"] = _rel(got, want)
+            res["grad_rel_vs_local"] = _rel(got, local[rank])      # no reduction at all
+            res["grad_rel_vs_sum"] = _rel(got, want * world)       # sum instead of average
         opt.step()
         losses.append(float(loss.item()))
     torch.cuda.synchronize()
@@ -151,8 +201,9 @@ def run_ddp(rank, world, dev, comm_kind, steps=3):
     idx = torch.arange(bits.numel(), device=dev, dtype=torch.int64)
     cs = int((bits * (idx % 8191 + 1)).sum().item())
     info = ddp.bucket_info()
-    return {"checksum": cs, "losses": losses, "finite": all(l == l for l in losses),
-            "native_comm": info["native_comm"], "xgmi": info["xgmi"]}
+    res.update({"checksum": cs, "losses": losses, "finite": all(l == l for l in losses),
+                "native_comm": info["native_comm"], "xgmi": info["xgmi"]})
+    return res
 
 
 def main():
@@ -178,8 +229,9 @@ def main():
         out["error"] = f"{type(e).__name__}: {e}"
         out["trace"] = traceback.format_exc()[-2000:]
     print("RESULT " + json.dumps(out), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
+    if dist.is_initialized():  # (a world-1 launch has no process group)
+        dist.barrier()
+        dist.destroy_process_group()
     sys.stdout.flush()
     os._exit(0 if out["status"] == "ok" else 1)
 

@@ -45,7 +45,10 @@ def _stage_cases():
             ("resnet18", 1, 64, 56, False), ("resnet18", 2, 64, 56, False), ("resnet18", 3, 128, 28, False),
             ("resnet18", 4, 256, 14, False),
             # PDT_BN_ACC path: epilogue-atomic sums, dgamma/dbeta in the apply, side-stream re-zero
-            ("resnet50", 1, 64, 56, True), ("resnet50", 3, 512, 28, True)]
+            ("resnet50", 1, 64, 56, True), ("resnet50", 3, 512, 28, True),
+            # deterministic mode (the reference's cudnn.deterministic=True): fixed-order partial
+            # sums, slab split-K weight gradients, and the folded BN backward on that path too
+            ("resnet50", 1, 64, 56, "det"), ("resnet50", 4, 1024, 14, "det")]
 
 
 @pytest.fixture(scope="module")
@@ -75,7 +78,9 @@ def models(gpu):
 @pytest.mark.parametrize("arch,stage,cin,hw,bn_acc", _stage_cases())
 def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc, monkeypatch):
     import pytorch_distributed_tutorials_amd.ops.fused as fused
-    monkeypatch.setattr(fused, "_BN_ACC", bn_acc)
+    import pytorch_distributed_tutorials_amd.utils.seed as seed
+    monkeypatch.setattr(fused, "_BN_ACC", bool(bn_acc))
+    monkeypatch.setattr(seed, "_DETERMINISTIC", bn_acc == "det")
     ref_model, nat_model, ddp = models[arch]
     layer_r = getattr(ref_model, f"layer{stage}")
     layer_n = getattr(nat_model, f"layer{stage}")
@@ -110,7 +115,7 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc
     torch.cuda.synchronize()
     # the folded BN backward (ops.fused DgradFold) runs in block 0's last unit of a Bottleneck pair
     # whenever the atomic BN sums are on
-    assert (fused.FOLD_CALLS > folds0) == (bn_acc and arch == "resnet50"), (fused.FOLD_CALLS, folds0)
+    assert (fused.FOLD_CALLS > folds0) == (bool(bn_acc) and arch == "resnet50"), (fused.FOLD_CALLS, folds0)
 
     errs, yard = {}, {}
     errs["out"] = _rel(out_n.permute(0, 3, 1, 2), out_r)
@@ -165,6 +170,41 @@ def _masked_block_fwd(block, x, masks):
         out = block.bn2(block.conv2(out))
     idn = block.downsample(x) if block.downsample is not None else x
     return (out + idn) * masks[-1]
+
+
+@pytest.mark.parametrize("stage,cin,hw", [(1, 64, 56), (3, 512, 28)])
+def test_block_pair_deterministic_bitwise(models, gpu, stage, cin, hw, monkeypatch):
+    """Deterministic mode, fold included: two forward + backward passes of the same block pair from
+    the same input give bit-identical outputs, input gradients and flat weight gradients."""
+    import pytorch_distributed_tutorials_amd.ops.fused as fused
+    import pytorch_distributed_tutorials_amd.utils.seed as seed
+    monkeypatch.setattr(seed, "_DETERMINISTIC", True)
+    _, nat_model, ddp = models["resnet50"]
+    blocks_n = [getattr(nat_model, f"layer{stage}")[i] for i in range(2)]
+    bn_n = [m for b in blocks_n for m in b.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    saved = [(m.running_mean.clone(), m.running_var.clone(), m.num_batches_tracked.clone()) for m in bn_n]
+    g = torch.Generator().manual_seed(31 + stage)
+    x = torch.relu(torch.randn(32, hw, hw, cin, generator=g)).to(torch.bfloat16).to(gpu)
+    runs = []
+    folds0 = fused.FOLD_CALLS
+    for _ in range(2):
+        ddp.space.grad_flat.zero_()
+        ddp.space.attach_grads()
+        x_n = x.clone().requires_grad_(True)
+        out = blocks_n[1].forward_native(blocks_n[0].forward_native(x_n))
+        dz = torch.randn(out.shape, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).to(gpu)
+        out.backward(dz)
+        torch.cuda.synchronize()
+        runs.append((out.detach().clone(), x_n.grad.clone(), ddp.space.grad_flat.clone()))
+        with torch.no_grad():
+            for m, (rm, rv, nbt) in zip(bn_n, saved):
+                m.running_mean.copy_(rm)
+                m.running_var.copy_(rv)
+                m.num_batches_tracked.copy_(nbt)
+    assert fused.FOLD_CALLS - folds0 == 2, "the folded BN backward must run in deterministic mode"
+    for a, b in zip(runs[0], runs[1]):
+        assert torch.equal(a, b)
+    assert runs[0][2].abs().sum() > 0
 
 
 @pytest.mark.parametrize("arch,stage,cin,hw,bn_acc", [c for c in _stage_cases() if not c[4]])

@@ -8,7 +8,8 @@ run one process per device -- ranks = min(device count, 8) -- and skip cleanly b
   reassociation, broadcast exact);
 * the direct xGMI backend with peer buffers on other GPUs: bitwise vs the rank-order fp32 sum,
   tiny unaligned buckets leave their neighbours alone, and the POISON protocol of a late peer;
-* native ResNet-18 DDP training over RCCL and over xGMI: every rank ends bit-identical.
+* native ResNet-18 DDP training over RCCL and over xGMI: every rank ends bit-identical, and the
+  step-1 averaged gradient matches the mean of the ranks' single-process gradients.
 Worker: tests/multigpu_worker.py.
 """
 import os
@@ -30,8 +31,8 @@ def _ndev():
 needs_two = pytest.mark.skipif(_ndev() < 2, reason="needs >= 2 GPUs (one process per device)")
 
 
-def _launch(mode, *extra, timeout=240):
-    n = min(_ndev(), 8)
+def _launch(mode, *extra, timeout=240, nproc=None):
+    n = nproc or min(_ndev(), 8)
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -79,3 +80,21 @@ def test_ddp_between_devices_ranks_bit_identical(comm):
     for x in res.values():
         assert x["finite"], x
         assert x["xgmi"] if comm == "xgmi" else x["native_comm"], x
+        # the averaged gradient is right (vs the mean of per-rank single-process native twins),
+        # and distinguishable from a reducer that did not average or did not reduce at all
+        assert x["grad_rel_vs_reference"] < 2e-2, x
+        assert x["grad_rel_vs_local"] > 5 * x["grad_rel_vs_reference"], x
+        assert x["grad_rel_vs_sum"] > 0.3, x
+
+
+def test_ddp_worker_gradient_reference_single_rank():
+    """The separate-device worker's gradient check itself, exercised on any GPU box: at world 1
+    the DDP gradient must equal the rank's own single-process gradient within tolerance (the
+    parameter-name mapping, the pre-re-layout state copy and the per-rank reference run)."""
+    if _ndev() < 1:
+        pytest.skip("needs a GPU")
+    n, res = _launch("ddp", "--comm", "auto", nproc=1)
+    x = res[0]
+    assert x["finite"], x
+    assert x["grad_rel_vs_reference"] < 2e-2, x
+    assert abs(x["grad_rel_vs_local"] - x["grad_rel_vs_reference"]) < 1e-6, x  # world 1: local == mean

@@ -119,6 +119,41 @@ def test_fwd_bn_fused_finalize_matches_partials(gpu, native_ext, shape, tile):
     assert _rel(y_b, yr) < 1e-2
 
 
+# (shape, input noise): pad 0 on the 3x3 so border pixels (fewer taps) do not widen the spread
+@pytest.mark.parametrize("shape,xnoise", [((16, 56, 56, 64, 256, 1, 1, 1, 0), 0.1),
+                                          ((64, 28, 28, 128, 256, 3, 3, 1, 0), 0.5)])
+def test_fwd_bn_fused_stats_far_from_zero_mean(gpu, native_ext, shape, xnoise):
+    """the fused statistics are E[y^2] - mean^2 from per-workgroup fp32 sums (fp64 only
+    across workgroups), so their error grows like (mean / std)^2.  Channels with |mean| / std of
+    roughly 10-100 (inputs offset from zero, weights with a per-channel offset): the fused invstd
+    and mean against an fp64 two-pass reference over the same bf16 y, and against the partials
+    path (per-wave M2 + Chan merge)."""
+    C = native_ext
+    n, h, w, c, k, r, s, st, pd = shape
+    g = torch.Generator().manual_seed(11)
+    x = (1.0 + xnoise * torch.randn(n, h, w, c, generator=g)).to(torch.bfloat16).to(gpu)
+    off = torch.linspace(0.01, 0.06, k).view(k, 1, 1, 1)  # per-output-channel weight offset
+    wt = (off + 0.01 * torch.randn(k, c, r, s, generator=g)).to(torch.bfloat16).float().to(gpu)
+    wt = wt.contiguous(memory_format=torch.channels_last)
+    M = n * ((h + 2 * pd - r) // st + 1) * ((w + 2 * pd - s) // st + 1)
+    wk = C.pack_weight(wt, c)
+    ones, zeros = torch.ones(k, device=gpu), torch.zeros(k, device=gpu)
+    y_p, st_p = C.conv_fwd_bn(x, wk, st, pd, M, zeros.clone(), ones.clone(), ones, zeros, 0.1, 1e-5)
+    acc = torch.zeros(8, 2, k, dtype=torch.float64, device=gpu)
+    y_f, st_f = C.conv_fwd_bn(x, wk, st, pd, M, zeros.clone(), ones.clone(), ones, zeros, 0.1, 1e-5, acc)
+    torch.cuda.synchronize()
+    assert torch.equal(y_p, y_f)
+    yd = y_f.double().reshape(-1, k)
+    mean_d = yd.mean(0)
+    var_d = (yd - mean_d).pow(2).mean(0)  # two-pass, fp64
+    ratio = (mean_d.abs() / var_d.sqrt()).float()
+    assert ratio.min() > 5 and ratio.max() > 30, ratio  # the regime the comment claims to cover
+    inv_d = torch.rsqrt(var_d + 1e-5).float()
+    assert torch.allclose(st_f[0], mean_d.float(), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(st_f[1], inv_d, rtol=1e-3), ((st_f[1] - inv_d).abs() / inv_d).max()
+    assert torch.allclose(st_p[1], inv_d, rtol=1e-3), ((st_p[1] - inv_d).abs() / inv_d).max()
+
+
 # dgrad GEMM (per parity class): M = N*H*W / stride^2, Nout = C, K_gemm = R*S*K
 DGRAD_TILES = [
     ((16, 56, 56, 256, 128, 1, 1, 1, 0), (128, 256)),   # short-K (K = 128): the 128x256 tile
