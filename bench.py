@@ -357,7 +357,7 @@ def main(argv=None) -> int:
     comm = None
     if args.impl == "native":
         info = ddp.bucket_info()
-        comm = {"native_comm": info["native_comm"], "reducer": info["reducer"], "xgmi": info["xgmi"],
+        comm = {"native_comm": info["native_comm"], "reducer": info["reducer"], "xgmi": info["xgmi"], "wgrad_cu_reserve": info.get("wgrad_cu_reserve", 0),
                 "buckets_mb": [round(b / 2**20, 2) for b in info["bucket_bytes"]]}
         # diagnostics for the scaling run (untimed, after the timed region): what the communicator
         # reports about itself, and one step's all-reduce time / exposed tail from the reducer's

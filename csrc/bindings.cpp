@@ -334,12 +334,19 @@ void bn_fold_wgrad(Tensor t1, Tensor gram, const Tensor& colsum, const Tensor& w
                    const std::optional<Tensor>& dgamma, const std::optional<Tensor>& dbeta,
                    const std::optional<Tensor>& done, bool zero_sums) {
   check_cuda(wt, "wt");
+  check_cuda(colsum, "colsum");
   TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.is_contiguous() && wt.numel() == wt.size(0) * wt.size(-1),
               "wt must be contiguous bf16 [C][K]");
   const int C = wt.size(0), K = wt.size(-1);
   TORCH_CHECK(t1.scalar_type() == at::kFloat && t1.numel() == (int64_t)K * C, "t1: fp32 [K, C]");
   TORCH_CHECK(gram.scalar_type() == at::kFloat && gram.numel() == (int64_t)C * C, "gram: fp32 [C, C]");
-  TORCH_CHECK(colsum.scalar_type() == at::kFloat && colsum.numel() >= C && colsum.is_contiguous(), "colsum: fp32 [C]");
+  // colsum: fp32 [C] (a reduction pass) or [S, C] (bn_act_fwd's S = bn_csum_slots() slots, consume
+  // mode: re-zeroed)
+  const int S = pdt::bn_csum_slots();
+  TORCH_CHECK(colsum.scalar_type() == at::kFloat && colsum.is_contiguous() &&
+              (colsum.numel() == C || (colsum.dim() == 2 && colsum.size(0) == S && colsum.size(1) == C)),
+              "colsum: fp32 [C] or [bn_csum_slots(), C]");
+  const int csum_slots = colsum.dim() == 2 ? S : 1;
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == (int64_t)K * C, "out: fp32 [K, C, 1, 1]");
   for (const Tensor* x : {(const Tensor*)&t1, (const Tensor*)&gram, (const Tensor*)&out}) {
     // 1x1: [K,C,1,1] in either memory format is [K][C] memory when its two big strides are (C, 1)
@@ -359,7 +366,7 @@ void bn_fold_wgrad(Tensor t1, Tensor gram, const Tensor& colsum, const Tensor& w
   pdt::launch_bn_fold_wgrad(t1.data_ptr<float>(), gram.data_ptr<float>(), colsum.data_ptr<float>(),
                             reinterpret_cast<const uint16_t*>(wt.data_ptr()), stats.data_ptr<float>(),
                             gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K, out.data_ptr<float>(),
-                            pg.first, pg.second, dp, zero_sums, cur_stream(wt));
+                            pg.first, pg.second, dp, zero_sums, cur_stream(wt), csum_slots);
 }
 
 // BN-fused dgrad of a 1x1 / stride-1 conv with the NEXT unit's BN backward folded in (kernels.h
@@ -826,7 +833,7 @@ static std::pair<const float*, const float*> res_bn_args(const std::optional<Ten
 
 Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
                   const std::optional<Tensor>& res, bool relu, const std::optional<Tensor>& rsc,
-                  const std::optional<Tensor>& rsh) {
+                  const std::optional<Tensor>& rsh, const std::optional<Tensor>& csum) {
   check_bf16_nhwc(y, "y");
   c10::hip::HIPGuard g(y.get_device());
   int K = y.size(3);
@@ -838,9 +845,17 @@ Tensor bn_act_fwd(const Tensor& y, const Tensor& scale, const Tensor& shift,
     rp = cbf(*res);
   }
   auto rbn = res_bn_args(res, rsc, rsh, K);
+  float* cs = nullptr;
+  if (csum.has_value() && csum->defined()) {  // per-channel sums of z into fp32 [S, K] slots (atomic)
+    check_cuda(*csum, "csum");
+    TORCH_CHECK(csum->scalar_type() == at::kFloat && csum->is_contiguous() &&
+                csum->numel() == (int64_t)pdt::bn_csum_slots() * K,
+                "csum must be a contiguous fp32 [bn_csum_slots(), K] device tensor");
+    cs = csum->data_ptr<float>();
+  }
   auto z = at::empty_like(y);
   pdt::launch_bn_act_fwd(cbf(y), scale.data_ptr<float>(), shift.data_ptr<float>(), rp, relu, bf(z), M,
-                         K, cur_stream(y), nullptr, rbn.first, rbn.second);
+                         K, cur_stream(y), nullptr, rbn.first, rbn.second, cs);
   return z;
 }
 
@@ -1486,7 +1501,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("eps"), py::arg("acc") = py::none());
   m.def("bn_act_fwd", checked("bn_act_fwd", &bn_act_fwd), py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("residual"), py::arg("relu"), py::arg("res_scale") = py::none(),
-        py::arg("res_shift") = py::none());
+        py::arg("res_shift") = py::none(), py::arg("csum") = py::none());
   m.def("bn_act_fwd_mask", checked("bn_act_fwd_mask", &bn_act_fwd_mask), py::arg("y"), py::arg("scale"),
         py::arg("shift"), py::arg("residual"), py::arg("res_scale") = py::none(),
         py::arg("res_shift") = py::none());
@@ -1560,6 +1575,10 @@ PYBIND11_MODULE(_C, m) {
     pdt::conv_nt_tile(M, Nout, kg_bytes, &bm, &bn);
     return py::make_tuple(bm, bn);
   }, py::arg("M"), py::arg("Nout"), py::arg("kg_bytes"));
+  m.def("bn_csum_slots", &pdt::bn_csum_slots, "slots of bn_act_fwd's column-sum accumulator");
+  m.def("conv_wgrad_set_cu_reserve", &pdt::conv_wgrad_set_cu_reserve, py::arg("n"),
+        "CUs the weight-gradient split-K plan leaves to the gradient-collective kernels");
+  m.def("conv_wgrad_cu_reserve", &pdt::conv_wgrad_cu_reserve);
   m.def("conv_wgrad_plan", [](std::vector<int64_t> x_shape, std::vector<int64_t> w_shape, int stride, int pad,
                               bool deterministic) {
     TORCH_CHECK(x_shape.size() == 4 && w_shape.size() == 4, "x_shape [N,H,W,C], w_shape [K,C,R,S]");

@@ -54,6 +54,8 @@ struct ReducerState {
 
   // LOCAL mode: one process, no communicator -- the optimizer-overlap stream only
   bool local = false;
+  bool tail_on_cur = false;  // this iteration's last bucket was updated on the caller's stream
+  bool tail_local = false;   // A/B: keep the last bucket on the overlap stream (PDT_TAIL_LOCAL=1)
   hipStream_t local_stream = nullptr;
   hipEvent_t ev_local = nullptr, ev_join = nullptr;
   // per-bucket fused SGD (optimizer in backward)
@@ -106,6 +108,20 @@ struct ReducerState {
       const int dev = params[0].get_device();
       c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
       hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+      if (b + 1 == (int64_t)flats.size() && !tail_local) {
+        // the last bucket (stem / layer-1 gradients, final at the very end of backward): its update
+        // runs on the caller's stream behind one wait for the side stream.  On the overlap stream it
+        // cost two unsatisfied cross-queue waits on the step's critical tail (overlap stream waits
+        // for the side stream, then the caller's stream for the overlap stream: ~50 us each, r9a)
+        if (aux) stream_handoff(aux, cur, ev_aux);
+        if (timing) {
+          hipEventRecord(ev_bwd, cur);
+          if (first) hipEventRecord(ev_start, cur);
+        }
+        apply_sgd(b, cur);
+        tail_on_cur = true;
+        return;
+      }
       stream_handoff(cur, local_stream, ev_local);
       if (aux) stream_handoff(aux, local_stream, ev_aux);
       if (timing && first) hipEventRecord(ev_start, local_stream);
@@ -227,13 +243,14 @@ struct ReducerState {
       const int dev = params[0].get_device();
       c10::hip::HIPGuard guard((c10::DeviceIndex)dev);
       hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
-      if (timing) {
-        hipEventRecord(ev_bwd, cur);
-        hipEventRecord(ev_end, local_stream);
+      if (timing && !tail_on_cur) hipEventRecord(ev_bwd, cur);
+      stream_handoff(local_stream, cur, ev_join);
+      if (timing) {  // every bucket's update done (the caller's stream joined the overlap stream)
+        hipEventRecord(ev_end, cur);
         timed = !launch_order.empty();
       }
-      stream_handoff(local_stream, cur, ev_join);
       }
+      tail_on_cur = false;
     } else if (xgmi) {
       if (timing) {
         c10::hip::HIPGuard guard((c10::DeviceIndex)xgmi->device());
@@ -319,6 +336,8 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<at::Tensor> grad_vi
   st_->reset_counters();
   if (const char* e = std::getenv("PDT_DEBUG_REDUCER")) st_->strict = e[0] == '1';
   if (const char* e = std::getenv("PDT_REDUCER_SKIP_COLL")) st_->skip_collectives = e[0] == '1';
+  // A/B (PDT_TAIL_LOCAL=1): the last bucket's update on the overlap stream like every other bucket
+  if (const char* e = std::getenv("PDT_TAIL_LOCAL")) st_->tail_local = e[0] == '1';
 
   std::weak_ptr<ReducerState> weak = st_;
   st_->self = weak;

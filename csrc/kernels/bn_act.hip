@@ -302,6 +302,8 @@ struct FoldCoef {
 };
 
 constexpr int kFoldMaxK = 2048;
+// bn_act_fwd's column-sum accumulator (CSUM, below): slots and grid cap
+constexpr int kCsumSlots = 128, kCsumBlocks = 4096;
 typedef __bf16 fold_v8bf __attribute__((ext_vector_type(8)));
 
 // Per-channel coefficients (a, b) of the fold into coef[2][K]: its own tiny launch so that the
@@ -439,7 +441,7 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ 
                                                             const uint16_t* __restrict__ wt, FoldCoef cf, int C,
                                                             float* __restrict__ out, float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, int* __restrict__ done,
-                                                            int zero_sums) {
+                                                            int zero_sums, int csum_slots) {
   const int K = cf.K, t = threadIdx.x;
   const int nc = C / kFoldTile;
   const int tk = blockIdx.x / nc, tc = blockIdx.x - tk * nc;
@@ -453,7 +455,22 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ 
   }
   __shared__ __attribute__((aligned(16))) float sW[32][kFoldTile];  // W^T chunk: [q][k]
   __shared__ __attribute__((aligned(16))) float sG[32][kFoldTile];  // Gram chunk: [q][c]
+  __shared__ float sCs[4][kFoldTile];  // column sums of this block's 64 columns (row 0 after the reduce)
   __shared__ int last;
+  {
+    const int j = t & (kFoldTile - 1), ph = t >> 6;  // column, slot phase (4 phases)
+    float a = 0.f;
+    if (csum_slots == 1) {
+      if (ph == 0) a = colsum[c0 + j];
+    } else {
+#pragma unroll 8
+      for (int sl = ph; sl < kCsumSlots; sl += 4) a += colsum[(size_t)sl * C + c0 + j];
+    }
+    sCs[ph][j] = a;
+    __syncthreads();
+    if (t < kFoldTile) sCs[0][t] = sCs[0][t] + sCs[1][t] + sCs[2][t] + sCs[3][t];
+    // (visible to every thread after the first barrier of the K loop below)
+  }
   const int ty = t >> 4, tx = t & 15;  // outputs (k0 + 4ty + i, c0 + 4tx + j)
   float acc[4][4] = {};
   for (int q0 = 0; q0 < C; q0 += 32) {
@@ -481,8 +498,10 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ 
     }
     __syncthreads();
   }
-  const float4 cs4 = *reinterpret_cast<const float4*>(colsum + c0 + tx * 4);
-  const float csv[4] = {cs4.x, cs4.y, cs4.z, cs4.w};
+  // colsum: one [C] vector (a reduction pass), or the forward apply's slots [kCsumSlots][C], summed
+  // into sCs by the whole block up front (4 threads per column, unrolled: a per-thread loop over
+  // 128 slots ran as 128 dependent L2 round trips, ~90 us per call)
+  const float csv[4] = {sCs[0][tx * 4], sCs[0][tx * 4 + 1], sCs[0][tx * 4 + 2], sCs[0][tx * 4 + 3]};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = k0 + ty * 4 + i;
@@ -522,6 +541,9 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ 
     const int q = e >> 4, cc = (e & 15) * 4;
     *reinterpret_cast<float4*>(gram + (size_t)q * C + c0 + cc) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  if (csum_slots > 1)  // forward-accumulated column sums: this group's columns of every slot
+    for (int e = t; e < csum_slots * kFoldTile; e += 256)
+      const_cast<float*>(colsum)[(size_t)(e / kFoldTile) * C + c0 + (e % kFoldTile)] = 0.f;
   if (last == 2 && zero_sums) {
     float* sm = const_cast<float*>(cf.sums);
     for (int e = t; e < 2 * K; e += 256) sm[e] = 0.f;
@@ -530,12 +552,15 @@ __global__ void __launch_bounds__(256) bn_fold_wgrad_kernel(float* __restrict__ 
 
 void launch_bn_fold_wgrad(float* t1, float* gram, const float* colsum, const uint16_t* wt,
                           const float* stats, const float* gamma, const float* sums, int M, int C, int K,
-                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st) {
+                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st,
+                          int csum_slots) {
   if (C % kFoldTile != 0 || K % kFoldTile != 0)
     throw std::runtime_error("bn_fold_wgrad: needs C % 64 == 0, K % 64 == 0");
+  if (csum_slots != 1 && (csum_slots != kCsumSlots || done == nullptr))
+    throw std::runtime_error("bn_fold_wgrad: column sums come as 1 vector, or bn_act_fwd's slots in consume mode");
   FoldCoef cf{stats, gamma, sums, K, 1.f / (float)M};
   hipLaunchKernelGGL(bn_fold_wgrad_kernel, dim3((K / kFoldTile) * (C / kFoldTile)), dim3(256), 0, st, t1, gram,
-                     colsum, wt, cf, C, out, dgamma, dbeta, done, zero_sums ? 1 : 0);
+                     colsum, wt, cf, C, out, dgamma, dbeta, done, zero_sums ? 1 : 0, csum_slots);
 }
 
 void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
@@ -574,7 +599,14 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 // shortcut of a downsampling block.  It is normalised here and rounded to bf16 exactly as a
 // separate apply pass would have stored it, so the block output is bit-identical to the unfused
 // path while the normalised shortcut is never written or read back (2 x |shortcut| of HBM).
-template <bool RES, bool RELU, bool MASK = false, bool RESBN = false, int U = 1>
+// CSUM: also the per-channel column sums of the stored bf16 z, fp32-atomically added into one of
+// kCsumSlots slots of csum[kCsumSlots][K] (the folded weight gradient's sum_m x, ops/fused.py
+// DgradFold: the unit's output is the next 1x1 conv's input, so its reduction pass on the
+// weight-gradient stream -- one 233 us launch at the end of layer 1 -- is gone).  Needs 256 % K8
+// == 0.  Same-address fp32 atomics serialise at the memory side (~0.15 us each): with 8 slots and
+// 8192 blocks the pass ran 155-204 us instead of 9-33 (r9s), so the grid is capped at
+// kCsumBlocks and the blocks spread over kCsumSlots slots (<= 32 atomics per address).
+template <bool RES, bool RELU, bool MASK = false, bool RESBN = false, int U = 1, bool CSUM = false>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift,
@@ -582,13 +614,16 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
                                                          uint4* __restrict__ z, int64_t nvec,
                                                          int K8, uint8_t* __restrict__ zmask = nullptr,
                                                          const float* __restrict__ rscale = nullptr,
-                                                         const float* __restrict__ rshift = nullptr) {
+                                                         const float* __restrict__ rshift = nullptr,
+                                                         float* __restrict__ csum = nullptr) {
   // the grid stride is a multiple of K8 (ew_blocks), so a thread's 8-channel group and its
   // scale/shift are fixed over the loop (no 64-bit modulo and 4 coefficient loads per vector)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(v0 % K8) * 8;
-  float sc[8], sh[8], rsc[8], rsh[8];
+  float sc[8], sh[8], rsc[8], rsh[8], cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
   load8(scale + c0, sc);
   load8(shift + c0, sh);
   if constexpr (RESBN) {
@@ -612,6 +647,11 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
     }
     const uint4 zb = pack8(a);
     z[v] = zb;
+    if constexpr (CSUM) {
+      const f8 zr = unpack8(zb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] += zr.v[j];
+    }
     if constexpr (MASK) {  // bit j = stored bf16 z > 0 (exactly what a z read would test)
       const f8 zr = unpack8(zb);
       uint32_t bits = 0;
@@ -636,6 +676,25 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const uint4* __restrict
     }
   }
   for (; v < nvec; v += stride) body(v, y[v], RES ? res[v] : uint4{});
+  if constexpr (CSUM) {
+    // threads t, t + K8, ... hold the same 8 channels (256 % K8 == 0): sum them in LDS, then one
+    // atomic per channel and block into this XCD's slot
+    __shared__ float red[256][9];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = cs[j];
+    __syncthreads();
+    if ((int)threadIdx.x < K8) {
+      float t8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t8[j] = 0.f;
+      for (int u = threadIdx.x; u < 256; u += K8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t8[j] += red[u][j];
+      float* slot = csum + (size_t)(blockIdx.x % kCsumSlots) * (K8 * 8) + threadIdx.x * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) unsafeAtomicAdd(slot + j, t8[j]);
+    }
+  }
 }
 
 // grid of an 8-channel-vector elementwise pass: at most kEwCap (kEwCapResidual for the residual
@@ -673,15 +732,29 @@ static void fwd_launch(dim3 g, dim3 b, hipStream_t st, const uint4* Y, const flo
                      zmask, rscale, rshift);
 }
 
+int bn_csum_slots() { return kCsumSlots; }
+
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
-                       hipStream_t st, uint8_t* zmask, const float* rscale, const float* rshift) {
+                       hipStream_t st, uint8_t* zmask, const float* rscale, const float* rshift,
+                       float* csum) {
   int64_t nvec = M * K / 8;
   int K8 = K / 8;
   dim3 g(ew_blocks(nvec, K8, res ? kEwCapResidual : kEwCap)), b(256);
   auto Y = reinterpret_cast<const uint4*>(y);
   auto R = reinterpret_cast<const uint4*>(res);
   auto Z = reinterpret_cast<uint4*>(z);
+  if (csum != nullptr) {
+    if (res || zmask || rscale || !relu || K8 > 256 || 256 % K8 != 0)
+      throw std::runtime_error("bn_act_fwd: column sums only on the plain BN+ReLU pass, 256 % (K/8) == 0");
+    // >= 8 vectors per thread: the atomics per block are fixed (K per block), so small tensors
+    // (layer 4: one vector per thread at the default grid) would be atomic-bound
+    const int64_t want = std::max<int64_t>(1, nvec / (256 * 8));
+    const dim3 gc(ew_blocks(std::min<int64_t>(nvec, want * 256), K8, kCsumBlocks));
+    hipLaunchKernelGGL((bn_act_fwd_kernel<false, true, false, false, 1, true>), gc, b, 0, st, Y, scale, shift,
+                       R, Z, nvec, K8, nullptr, nullptr, nullptr, csum);
+    return;
+  }
   if (rscale != nullptr) {  // residual = BN(raw shortcut conv output), normalised on the fly
     if (!res || !rshift) throw std::runtime_error("bn_act_fwd: residual BN needs the residual and its shift");
     if (zmask) {

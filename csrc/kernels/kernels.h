@@ -132,7 +132,8 @@ void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float*
 // their next use (done: an int completion counter, 0 between launches)
 void launch_bn_fold_wgrad(float* t1, float* gram, const float* colsum, const uint16_t* wt,
                           const float* stats, const float* gamma, const float* sums, int M, int C, int K,
-                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st);
+                          float* out, float* dgamma, float* dbeta, int* done, bool zero_sums, hipStream_t st,
+                          int csum_slots = 1);  // bn_csum_slots(): bn_act_fwd's [slots][C], re-zeroed here
 void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, const uint16_t* addend,
                        const ConvShape& s, hipStream_t st, const BnBwdFuse* bn = nullptr,
                        int addend_sub = 0, const DgradFold* fold = nullptr);
@@ -141,6 +142,9 @@ void launch_conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, con
 size_t conv_wgrad_ws_floats(const ConvShape& s, bool deterministic);
 // the weight-gradient launch plan: {tile rows (output channels), tile cols, tiles, split-K factor}
 void conv_wgrad_plan(const ConvShape& s, bool deterministic, int out[4]);
+// CUs the weight-gradient split-K plan leaves free for collective kernels (0: plan the whole chip)
+void conv_wgrad_set_cu_reserve(int n);
+int conv_wgrad_cu_reserve();
 // accumulate: dw += wgrad (autograd accumulation semantics; lets the block write straight into
 // the flat gradient buffer), else dw = wgrad.
 // fp8 weight gradient: dw[K][R][S][C] (+)= wgrad(dy8 e5m2 [N,Ho,Wo,K] * dy_deq, x8 e4m3 [N,H,W,C] * x_deq),
@@ -173,7 +177,8 @@ void launch_bn_eval_params(const float* rm, const float* rv, const float* gamma,
 void launch_bn_act_fwd(const uint16_t* y, const float* scale, const float* shift,
                        const uint16_t* res, bool relu, uint16_t* z, int64_t M, int K,
                        hipStream_t st, uint8_t* zmask = nullptr, const float* rscale = nullptr,
-                       const float* rshift = nullptr);
+                       const float* rshift = nullptr, float* csum = nullptr);  // csum: [bn_csum_slots()][K]
+int bn_csum_slots();
 // Backward BN.  stats = bn_finalize output [4][K] (mean, invstd, scale, shift).  mask: 0 = no
 // ReLU, 1 = ReLU mask from z (> 0), 2 = ReLU mask recomputed from y (y*scale + shift > 0).
 // sums[2][K] = (sum g, sum g*(y-mean)) with g = dz * mask; ws >= bn_bwd_ws_floats(M, K)

@@ -667,8 +667,19 @@ struct WgPlan {
   bool slab;                    // split-K partials in private slabs + fixed-order reduce (else atomics)
 };
 
-// CUs the split-K plan fills: the device's (measured in-step, one MI355X, atomic split-K: planning
-// for 128 or 256 CUs gave the same step, 96 was 1.2 % slower).
+// CUs the split-K plan fills: the device's, minus a reserve for the gradient-collective kernels
+// when the step all-reduces (measured in-step at world 1, one MI355X, atomic split-K: planning
+// for 128 or 256 CUs gave the same step, 96 was 1.2 % slower, r5: 224 vs 256 +0.2 %).  A weight-
+// gradient block holds its CU's LDS and registers for the whole of its K range (one 512-thread
+// block per CU), so with a grid of >= CUs blocks an RCCL channel block or an xGMI data kernel
+// launched beside it waits for a whole wgrad kernel -- and every peer rank's channel spins
+// meanwhile.  A plan of at most (CUs - reserve) blocks per round keeps the reserve free for them
+// (a soft reservation: the hardware dispatcher places blocks anywhere; grids above the plan's
+// budget still fill the chip).  Set by the DDP wrapper (conv_wgrad_set_cu_reserve).
+static int g_wg_reserve = 0;
+void conv_wgrad_set_cu_reserve(int n) { g_wg_reserve = n < 0 ? 0 : n; }
+int conv_wgrad_cu_reserve() { return g_wg_reserve; }
+
 static int wg_cus() {
   static int v = -1;
   if (v < 0) {
@@ -678,7 +689,7 @@ static int wg_cus() {
     else
       v = 256;
   }
-  return v;
+  return std::max(v / 2, v - g_wg_reserve);
 }
 
 // Split-K factor: one 512-thread block per CU at a time, so a plan of tiles * splits blocks runs

@@ -64,12 +64,12 @@ class BasicBlock(nn.Module):
             identity = self.downsample(x)
         return self.relu(out + identity)
 
-    def forward_native(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_native(self, x: torch.Tensor, tail: bool = False) -> torch.Tensor:
         if x.is_cuda:  # one fused autograd node per block on the device path
             m = self._modules  # direct dict reads: nn.Module.__getattr__ is a slow fallback path
             d = m.get("downsample")  # None is a plain attribute, not in _modules
             ds = (d[0], d[1]) if d is not None else None
-            return ops.residual_block(x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"])], ds)
+            return ops.residual_block(x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"])], ds, tail)
         out = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
         identity = x
         if self.downsample is not None:
@@ -103,13 +103,13 @@ class Bottleneck(nn.Module):
             identity = self.downsample(x)
         return self.relu(out + identity)
 
-    def forward_native(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_native(self, x: torch.Tensor, tail: bool = False) -> torch.Tensor:
         if x.is_cuda:  # one fused autograd node per block on the device path
             m = self._modules  # direct dict reads: nn.Module.__getattr__ is a slow fallback path
             d = m.get("downsample")  # None is a plain attribute, not in _modules
             ds = (d[0], d[1]) if d is not None else None
             return ops.residual_block(
-                x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"]), (m["conv3"], m["bn3"])], ds)
+                x, [(m["conv1"], m["bn1"]), (m["conv2"], m["bn2"]), (m["conv3"], m["bn3"])], ds, tail)
         identity = x
         if self.downsample is not None:
             identity = ops.conv_bn(x, self.downsample[0], self.downsample[1], relu=False)
@@ -205,9 +205,10 @@ class ResNet(nn.Module):
             x = ops.conv_bn(x, self.conv1, self.bn1, relu=True)
             x = ops.maxpool3x3s2(x)
         x = ops.fp8_attach(x, self.maxpool)  # e4m3 copy for fp8 convs (no-op unless ops.set_fp8)
+        last = self.layer4[len(self.layer4) - 1]
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
-                x = blk.forward_native(x)
+                x = blk.forward_native(x, blk is last)  # the tail block hands no BN backward on
         return ops.avgpool_linear(x, self.fc.weight, self.fc.bias)
 
 

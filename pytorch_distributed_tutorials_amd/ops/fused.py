@@ -760,12 +760,13 @@ def _packed_crsk(w):
 
 
 def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentum, eps, residual,
-              x8=None, q8=None, want_mask=False, want_z=True):
+              x8=None, q8=None, want_mask=False, want_z=True, csum=None):
     """conv -> BN -> (+residual) -> (ReLU) -> (z, y, stats, z8, zmask).  x8 = (e4m3 copy of x, its
     dequant factor): fp8 conv; q8 = _Q8State: also emit the e4m3 copy z8 of the output;
     want_mask (with relu): also the 1-bit ReLU mask zmask a later BN-fused dgrad reads instead of z.
     ``residual`` is an activation, or ``(y_short, stats_short)``: a projection shortcut's raw conv
-    output and its BN statistics, normalised inside this unit's apply pass (never materialised)."""
+    output and its BN statistics, normalised inside this unit's apply pass (never materialised).
+    csum: fp32 [8, k] slots the apply adds the output's per-channel sums into (DgradFold colsum)."""
     y, stats = _unit_conv_stats(C, x, w, gamma, beta, rm, rv, stride, pad, training, momentum, eps, x8)
     k = w.shape[0]
     rsc = rsh = None
@@ -781,7 +782,7 @@ def _unit_fwd(C, x, w, gamma, beta, rm, rv, stride, pad, relu, training, momentu
     if want_mask:
         z, zm = C.bn_act_fwd_mask(y, stats[2], stats[3], residual, rsc, rsh)
         return z, y, stats, None, zm
-    z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu, rsc, rsh)
+    z = C.bn_act_fwd(y, stats[2], stats[3], residual, relu, rsc, rsh, csum)
     return z, y, stats, None, None
 
 
@@ -885,7 +886,7 @@ class _ResidualBlock(torch.autograd.Function):
         _nan_trace(f"block-in {tuple(x.shape)}", x=x)
         if _LEAD is not None:
             _lead_mark(f"fwd {tuple(x.shape)}")
-        chain, ds_cfg = spec
+        chain, ds_cfg, spec_tail = spec
         nch = len(chain)
         saved = [x]
         # fp8io = (x8, per-chain-unit _Q8State list, holder for the output's e4m3 copy) or None
@@ -918,6 +919,10 @@ class _ResidualBlock(torch.autograd.Function):
         outs = []
         ins8 = [x8]  # e4m3 copy (q, dequant factor) of each chain unit's conv input, or None
         zmask = None
+        # the last unit's folded weight gradient needs sum_m of its conv input: summed by the apply
+        # that writes that input (no reduction pass in backward)
+        csum = _csum_for(chain, tensors, x) if not spec_tail and fp8io is None else None
+        ctx.colsum = csum
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
             last = i == nch - 1
@@ -929,7 +934,7 @@ class _ResidualBlock(torch.autograd.Function):
             z, y, stt, h8, zm = _unit_fwd(C, h, w, g, b, rm, rv, st, pd, True, tr, mo, ep,
                                           res if last else None, h8, q8s[i] if q8s else None,
                                           want_mask=last and tr and _ZMASK and _BN_HANDOFF and _FUSE_DGRAD_BN,
-                                          want_z=want_z)
+                                          want_z=want_z, csum=csum if i == nch - 2 else None)
             if z is None and h8 is None:
                 raise RuntimeError("fp8-only activation without its e4m3 copy")
             if last:
@@ -964,7 +969,7 @@ class _ResidualBlock(torch.autograd.Function):
         C = native()
         if _LEAD is not None:
             _lead_mark(f"bwd {tuple(dz.shape)}")
-        chain, ds_cfg = ctx.spec
+        chain, ds_cfg, _ = ctx.spec
         nch = len(chain)
         sv = ctx.saved_tensors
         x = sv[0]
@@ -1175,7 +1180,10 @@ class _ResidualBlock(torch.autograd.Function):
                     t1, gram, done = _fold_ws(k_, c_, xin.device)
                     C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, det, t1)
                     C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, det, gram)
-                    colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
+                    colsum = ctx.colsum if not det else None
+                    if colsum is None:
+                        colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
+                    ctx.colsum = None  # consumed: bn_fold_wgrad re-zeroes the [S, C] slots
                     dfr = deferred.pop(5 * i, None)
                     C.bn_fold_wgrad(t1, gram, colsum, wt.view(c_, k_), stt, gamma, sums, count,
                                     _grad_sink(params[5 * i]), dfr[1] if dfr is not None else None,
@@ -1243,6 +1251,9 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.handoff_in = None
         for acc_, _, _ in deferred.values():  # (every unit's weight gradient re-zeroes its own)
             acc_.zero_()
+        if ctx.colsum is not None:  # summed in forward but not folded (no hand-off into this block)
+            ctx.colsum.zero_()
+            ctx.colsum = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
         return (dz, None, None, None, *grads)
@@ -1271,6 +1282,28 @@ def _fold_ok(i, last, w, xin, st, pd, tr, det, side, fp8b, params) -> bool:
     j = 5 * (i - 1)
     return (_grad_sink(params[j + 1]) is not None and _grad_sink(params[j + 2]) is not None
             and _grad_sink(params[5 * i]) is not None)
+
+
+def _csum_for(chain, tensors, x):
+    """The [S, C] fp32 column-sum slots (S = C.bn_csum_slots()) the apply of the unit before the last fills for the folded
+    weight gradient (zeroed; bn_fold_wgrad re-zeroes them after use), or None where the fold cannot
+    run (the static half of _fold_ok: a training bottleneck whose last conv is a foldable 1x1, bf16,
+    not deterministic -- the sums are fp32 atomics -- with a weight-gradient side stream)."""
+    nch = len(chain)
+    if nch < 2 or not x.is_cuda or deterministic() or _FP8 or not (_FOLD_BN and _BN_ACC and _FUSE_DGRAD_BN):
+        return None
+    st, pd, tr, _, _ = chain[-1]
+    w = tensors[5 * (nch - 1)]
+    k, c, r, s_ = w.shape
+    if not tr or r != 1 or s_ != 1 or st != 1 or pd != 0 or k % 256 or k > 2048 or c % 64 or 256 % (c // 8):
+        return None
+    if streams.wgrad_stream(x.device) is None or _grad_sink(w) is None:
+        return None
+    cs = getattr(w, "_pdt_csum", None)
+    if cs is None or cs.shape[1] != c or cs.device != x.device:
+        cs = torch.zeros(native().bn_csum_slots(), c, dtype=torch.float32, device=x.device)
+        w._pdt_csum = cs
+    return cs
 
 
 _ZSTATS = {}
@@ -1312,9 +1345,11 @@ def _unit_tensors(conv: nn.Conv2d, bn: nn.BatchNorm2d) -> list:
     return [conv._parameters["weight"], bp["weight"], bp["bias"], bb["running_mean"], bb["running_var"]]
 
 
-def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
+def residual_block(x: torch.Tensor, chain, downsample=None, tail: bool = False) -> torch.Tensor:
     """Device path of a ResNet block: ``chain`` = [(conv, bn), ...] (ReLU after each BN, the
-    shortcut added before the last ReLU), ``downsample`` = (conv, bn) or None."""
+    shortcut added before the last ReLU), ``downsample`` = (conv, bn) or None.  ``tail``: the
+    network's last block (no next block hands its last BN backward into this one, so its
+    folded weight gradient cannot run and the forward takes no column sums for it)."""
     spec_chain, tensors = [], []
     for conv, bn in chain:
         tr, mo, ep = _bn_prepare(bn)
@@ -1330,7 +1365,7 @@ def residual_block(x: torch.Tensor, chain, downsample=None) -> torch.Tensor:
     if _FP8:
         q8s = [_q8_state(bn, x.device) for _, bn in chain]
         fp8io = (getattr(x, "_pdt_fp8", None), q8s, [])
-    out = _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec), getattr(x, "_pdt_handoff", None),
+    out = _ResidualBlock.apply(x, (tuple(spec_chain), ds_spec, tail), getattr(x, "_pdt_handoff", None),
                                fp8io, *tensors)
     node = out.grad_fn  # the ctx of this block's node (None without autograd)
     if node is not None and getattr(node, "handoff_out", None) is not None:

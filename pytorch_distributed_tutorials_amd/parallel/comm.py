@@ -94,13 +94,18 @@ class CommOptions:
     ``max_channels`` bound the RCCL channels (rings) a collective spreads over (``ncclConfig_t``
     minCTAs / maxCTAs; 0 = RCCL's choice); the env knob ``PDT_RCCL_CHANNELS=min[,max]`` sets them
     too.  ``xgmi_blocks`` is the same budget for the direct xGMI backend: its reduce-scatter /
-    all-gather kernels use at most that many workgroups beside the backward pass."""
+    all-gather kernels use at most that many workgroups beside the backward pass.
+    ``wgrad_cu_reserve``: CUs the weight-gradient split-K plan leaves free for those collective
+    kernels while the step all-reduces across ranks (-1 = auto: the xGMI block budget, or the RCCL
+    channel cap, 32 when RCCL chooses; env ``PDT_WGRAD_RESERVE_CUS``; ``DistributedDataParallel``
+    applies it)."""
     init_timeout: float = DEFAULT_TIMEOUT_S
     op_timeout: float = DEFAULT_TIMEOUT_S
     exit_on_error: Optional[bool] = None
     min_channels: int = 0
     max_channels: int = 0
     xgmi_blocks: int = 16  # CU budget of the xGMI backend's data kernels (PDT_XGMI_BLOCKS)
+    wgrad_cu_reserve: int = -1
 
     @classmethod
     def from_env(cls, timeout: Optional[float] = None, **kw) -> "CommOptions":
@@ -112,6 +117,8 @@ class CommOptions:
             o.init_timeout = o.op_timeout = float(os.environ["PDT_COMM_TIMEOUT"])
         if os.environ.get("PDT_XGMI_BLOCKS"):
             o.xgmi_blocks = max(1, int(os.environ["PDT_XGMI_BLOCKS"]))
+        if os.environ.get("PDT_WGRAD_RESERVE_CUS"):
+            o.wgrad_cu_reserve = max(0, int(os.environ["PDT_WGRAD_RESERVE_CUS"]))
         ch = os.environ.get("PDT_RCCL_CHANNELS")
         if ch and not (o.min_channels or o.max_channels):
             parts = [int(x) for x in ch.split(",")]
@@ -249,3 +256,15 @@ def destroy() -> None:
     _COMM_CACHE.clear()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def wgrad_cu_reserve(opts: CommOptions, xgmi: bool, collective_world: int) -> int:
+    """CUs to keep out of the weight-gradient split-K plan (csrc/kernels/wgrad.hip wg_cus): none
+    unless gradients are all-reduced across ranks (or a world-1 run rehearses a larger world)."""
+    if opts.wgrad_cu_reserve >= 0:
+        return opts.wgrad_cu_reserve
+    if collective_world <= 1:
+        return 0
+    if xgmi:
+        return opts.xgmi_blocks
+    return opts.max_channels if opts.max_channels > 0 else 32

@@ -247,6 +247,15 @@ class DistributedDataParallel(nn.Module):
                 if comm == "rccl":
                     raise
                 warnings.warn(f"{e}; gradients are reduced through torch.distributed collectives")
+        # CUs the weight-gradient kernels leave to the collective kernels that overlap backward
+        # (a process-wide plan setting: one DDP wrapper per process)
+        self.wgrad_cu_reserve = 0
+        if self.device.type == "cuda" and native_available():
+            from ..ops._ext import native
+            self.wgrad_cu_reserve = pcomm.wgrad_cu_reserve(
+                self.comm_options, self.xgmi is not None,
+                self.plan_world if self._collective and (self.comm is not None or self.xgmi is not None) else 1)
+            native().conv_wgrad_set_cu_reserve(self.wgrad_cu_reserve)
         # the buffer-broadcast wait can move to the first BatchNorm only where every buffer
         # reader is one of our BN kernels (ops.buffers_ready): the native device model
         self._defer_buffer_wait = self.comm is not None and getattr(module, "impl", None) == "native"
@@ -461,5 +470,6 @@ class DistributedDataParallel(nn.Module):
         return {"num_buckets": len(self.bucket_ranges), "bucket_elems": list(self.bucket_sizes),
                 "bucket_bytes": list(self.bucket_bytes),
                 "native_comm": self.comm is not None, "forced": self.force_reducer,
+                "wgrad_cu_reserve": getattr(self, "wgrad_cu_reserve", 0),
                 "xgmi": self.xgmi is not None,
                 "reducer": type(self.reducer).__name__ if self.reducer is not None else None}

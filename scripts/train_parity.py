@@ -63,11 +63,19 @@ def main():
     ap.add_argument("--fp8-parts", default="all", choices=["all", "fwd", "fwd+dgrad"],
                     help="diagnostics: which GEMMs take fp8 (forward only / + input gradients / + weight "
                          "gradients)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="native side in deterministic mode (the reference's cudnn.deterministic=True: "
+                         "fixed-order reductions, slab split-K weight gradients): one run is reproducible "
+                         "bit for bit, so a single-run criterion tests the trajectory, not one draw of noise")
     ap.add_argument("--repeats", type=int, default=1,
                     help="native runs from the same init and data order (stock runs once); the JSON's "
                          "native curve is their mean, the single runs are listed too")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.deterministic:
+        from pytorch_distributed_tutorials_amd.utils.seed import set_random_seeds
+        set_random_seeds(0, deterministic=True)
+        torch.backends.cudnn.enabled = False  # (set_random_seeds flips cudnn flags; keep MIOpen off)
     if a.fp8:
         ops.set_fp8(True)
         from pytorch_distributed_tutorials_amd.ops import fused
@@ -131,6 +139,7 @@ def main():
         "stock_train_acc": accuracy(stock, ds, False),
         "finite": bool(all(torch.isfinite(r).all() for r in runs) and torch.isfinite(ls).all()),
         "repeats": a.repeats,
+        "deterministic": bool(a.deterministic),
     }
     line = json.dumps(res)
     print(line, flush=True)

@@ -121,6 +121,27 @@ def test_conv_wgrad(gpu, native_ext, shape, deterministic):
     assert _rel_err(dw, dwr) < 1e-2
 
 
+@pytest.mark.parametrize("nhwk", [(16, 56, 56, 64), (8, 28, 28, 128), (8, 14, 14, 256), (4, 7, 7, 512), (3, 5, 7, 64)])
+def test_bn_act_fwd_column_sums(gpu, native_ext, nhwk):
+    """bn_act_fwd(csum=): the same z bit for bit, and per-channel sums of the STORED bf16 z added into
+    C.bn_csum_slots() fp32 slots (accumulating over calls: the consumer re-zeroes them) -- the folded weight
+    gradient's sum_m x, against an fp64 sum of z."""
+    C = native_ext
+    g = torch.Generator().manual_seed(21)
+    n, h, w, k = nhwk
+    y = torch.randn(n, h, w, k, generator=g).to(torch.bfloat16).to(gpu)
+    scale = (torch.rand(k, generator=g) + 0.5).to(gpu)
+    shift = (0.2 * torch.randn(k, generator=g)).to(gpu)
+    z0 = C.bn_act_fwd(y, scale, shift, None, True)
+    cs = torch.zeros(C.bn_csum_slots(), k, device=gpu)
+    z1 = C.bn_act_fwd(y, scale, shift, None, True, None, None, cs)
+    assert torch.equal(z0, z1)
+    want = z0.double().sum((0, 1, 2))
+    assert torch.allclose(cs.double().sum(0), want, rtol=1e-5, atol=1e-3), (cs.sum(0) - want).abs().max()
+    C.bn_act_fwd(y, scale, shift, None, True, None, None, cs)  # accumulates
+    assert torch.allclose(cs.double().sum(0), 2 * want, rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("relu,res,nhwk", [
     (True, False, (4, 7, 9, 128)), (True, True, (4, 7, 9, 128)), (False, False, (4, 7, 9, 128)),
     # channel-chunked reduction grid (K8 > 32) and a many-row-block case
