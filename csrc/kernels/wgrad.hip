@@ -78,7 +78,10 @@ struct WgCfg {
   static constexpr int A_ROWB = BM * 2, B_ROWB = BN * 2;   // bytes per pixel row of each image
   static constexpr int A_BYTES = 64 * A_ROWB, B_BYTES = 64 * B_ROWB;
   static constexpr int STAGE = A_BYTES + B_BYTES;          // 32 KB (2x2) or 40 KB (1x4, 4x1)
-  static constexpr int STAGES = 4;
+#ifndef PDT_WG_STAGES
+#define PDT_WG_STAGES 4
+#endif
+  static constexpr int STAGES = PDT_WG_STAGES;             // (>= 3: fragments are read one step ahead)
   static constexpr int SMEM = STAGES * STAGE;              // 128 or 160 KB: one block per CU
   static_assert(SMEM <= 163840, "LDS");
   static constexpr int A_LPR = A_ROWB / 16, A_RPI = 64 / A_LPR;  // lanes per row / rows per piece

@@ -921,7 +921,9 @@ class _ResidualBlock(torch.autograd.Function):
         zmask = None
         # the last unit's folded weight gradient needs sum_m of its conv input: summed by the apply
         # that writes that input (no reduction pass in backward)
-        csum = _csum_for(chain, tensors, x) if not spec_tail and fp8io is None else None
+        fold_fwd = not spec_tail and fp8io is None and _fold_colsum_ok(chain, tensors, x)
+        det_fwd = deterministic()
+        csum = _csum_slots(tensors[5 * (nch - 1)], x.device) if fold_fwd and not det_fwd else None
         ctx.colsum = csum
         for i, (st, pd, tr, mo, ep) in enumerate(chain):
             w, g, b, rm, rv = tensors[5 * i:5 * i + 5]
@@ -937,6 +939,14 @@ class _ResidualBlock(torch.autograd.Function):
                                           want_z=want_z, csum=csum if i == nch - 2 else None)
             if z is None and h8 is None:
                 raise RuntimeError("fp8-only activation without its e4m3 copy")
+            if fold_fwd and det_fwd and i == nch - 2:
+                # deterministic runs (no atomics): the fixed-order column-sum reduction of the last
+                # unit's conv input runs here, on the weight-gradient stream -- idle during the
+                # forward -- instead of at the end of backward, where that stream is the tail
+                side = streams.wgrad_stream(z.device)
+                streams.fork(side, z)
+                with torch.cuda.stream(side):
+                    ctx.colsum = C.bn_act_bwd_reduce(z, z, z, _zero_stats(z.shape[3], z.device), 0)[0]
             if last:
                 zmask = zm
             else:
@@ -1180,7 +1190,7 @@ class _ResidualBlock(torch.autograd.Function):
                     t1, gram, done = _fold_ws(k_, c_, xin.device)
                     C.conv_wgrad(g, xin, [k_, c_, 1, 1], 1, 0, det, t1)
                     C.conv_wgrad(xin, xin, [c_, c_, 1, 1], 1, 0, det, gram)
-                    colsum = ctx.colsum if not det else None
+                    colsum = ctx.colsum  # forward: [S, C] atomic slots, or (deterministic) [C] sums
                     if colsum is None:
                         colsum = C.bn_act_bwd_reduce(xin, xin, xin, _zero_stats(c_, xin.device), 0)[0]
                     ctx.colsum = None  # consumed: bn_fold_wgrad re-zeroes the [S, C] slots
@@ -1252,7 +1262,8 @@ class _ResidualBlock(torch.autograd.Function):
         for acc_, _, _ in deferred.values():  # (every unit's weight gradient re-zeroes its own)
             acc_.zero_()
         if ctx.colsum is not None:  # summed in forward but not folded (no hand-off into this block)
-            ctx.colsum.zero_()
+            if ctx.colsum.dim() == 2:  # the atomic slots must be left zeroed
+                ctx.colsum.zero_()
             ctx.colsum = None
         if sunk:
             sunk[0]._pdt_flat.mark_ready(sunk)
@@ -1284,24 +1295,28 @@ def _fold_ok(i, last, w, xin, st, pd, tr, det, side, fp8b, params) -> bool:
             and _grad_sink(params[5 * i]) is not None)
 
 
-def _csum_for(chain, tensors, x):
-    """The [S, C] fp32 column-sum slots (S = C.bn_csum_slots()) the apply of the unit before the last fills for the folded
-    weight gradient (zeroed; bn_fold_wgrad re-zeroes them after use), or None where the fold cannot
-    run (the static half of _fold_ok: a training bottleneck whose last conv is a foldable 1x1, bf16,
-    not deterministic -- the sums are fp32 atomics -- with a weight-gradient side stream)."""
+def _fold_colsum_ok(chain, tensors, x) -> bool:
+    """Will the last unit's folded weight gradient (DgradFold) want sum_m of its conv input?  The
+    static half of _fold_ok: a training bottleneck whose last conv is a foldable 1x1, bf16, with a
+    weight-gradient side stream and a flat-space gradient sink."""
     nch = len(chain)
-    if nch < 2 or not x.is_cuda or deterministic() or _FP8 or not (_FOLD_BN and _BN_ACC and _FUSE_DGRAD_BN):
-        return None
+    if nch < 2 or not x.is_cuda or _FP8 or not (_FOLD_BN and _BN_ACC and _FUSE_DGRAD_BN):
+        return False
     st, pd, tr, _, _ = chain[-1]
     w = tensors[5 * (nch - 1)]
     k, c, r, s_ = w.shape
     if not tr or r != 1 or s_ != 1 or st != 1 or pd != 0 or k % 256 or k > 2048 or c % 64 or 256 % (c // 8):
-        return None
-    if streams.wgrad_stream(x.device) is None or _grad_sink(w) is None:
-        return None
+        return False
+    return streams.wgrad_stream(x.device) is not None and _grad_sink(w) is not None
+
+
+def _csum_slots(w, dev):
+    """The zeroed [S, C] fp32 column-sum slots (S = C.bn_csum_slots()) the apply of the unit before
+    the last atomically fills (bn_fold_wgrad re-zeroes them after use), one set per folded conv."""
+    c = w.shape[1]
     cs = getattr(w, "_pdt_csum", None)
-    if cs is None or cs.shape[1] != c or cs.device != x.device:
-        cs = torch.zeros(native().bn_csum_slots(), c, dtype=torch.float32, device=x.device)
+    if cs is None or cs.shape[1] != c or cs.device != dev:
+        cs = torch.zeros(native().bn_csum_slots(), c, dtype=torch.float32, device=dev)
         w._pdt_csum = cs
     return cs
 
