@@ -97,7 +97,7 @@ class CommOptions:
     all-gather kernels use at most that many workgroups beside the backward pass.
     ``wgrad_cu_reserve``: CUs the weight-gradient split-K plan leaves free for those collective
     kernels while the step all-reduces across ranks (-1 = auto: the xGMI block budget, or the RCCL
-    channel cap, 32 when RCCL chooses; env ``PDT_WGRAD_RESERVE_CUS``; ``DistributedDataParallel``
+    channel cap, 16 when RCCL chooses; env ``PDT_WGRAD_RESERVE_CUS``; ``DistributedDataParallel``
     applies it)."""
     init_timeout: float = DEFAULT_TIMEOUT_S
     op_timeout: float = DEFAULT_TIMEOUT_S
@@ -267,4 +267,4 @@ def wgrad_cu_reserve(opts: CommOptions, xgmi: bool, collective_world: int) -> in
         return 0
     if xgmi:
         return opts.xgmi_blocks
-    return opts.max_channels if opts.max_channels > 0 else 32
+    return opts.max_channels if opts.max_channels > 0 else 16
