@@ -208,13 +208,19 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& w, std::vector<int64_t> xs, in
 // bn_act_bwd_reduce.  bn_act_bwd_apply(g, ..., mask=0) then yields that unit's dy.
 // shared body of conv_dgrad_bn / conv_dgrad_bn_fp8: `launch(s, dx, addend, bn, stream)` runs the
 // BN-fused dgrad
+// optional second BN on the same gradient (kernels.h BnBwdFuse::y2): a downsampling block's
+// projection-shortcut BN, reduced by the same epilogue into its own [2][C] accumulator
+struct SecondBn {
+  std::optional<Tensor> y, stats, acc;
+};
+
 template <typename Launch>
 std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvShape& s,
                                          const std::optional<Tensor>& addend, const Tensor& y,
                                          const std::optional<Tensor>& z, const Tensor& stats, int64_t mask,
                                          const std::optional<Tensor>& dgamma,
                                          const std::optional<Tensor>& dbeta, const std::optional<Tensor>& acc,
-                                         Launch&& launch) {
+                                         const SecondBn& bn2, Launch&& launch) {
   check_bf16_nhwc(y, "y");
   TORCH_CHECK(y.size(0) == s.N && y.size(1) == s.H && y.size(2) == s.W && y.size(3) == s.C,
               "dgrad_bn: y must have the shape of x");
@@ -249,6 +255,19 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
                 acc->numel() == 2 * s.C, "acc must be a contiguous fp32 [2, C] device tensor");
     TORCH_CHECK(!(dgamma.has_value() && dgamma->defined()), "acc mode: pass dgamma/dbeta to the apply");
     pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), nullptr, (int)mask, acc->data_ptr<float>()};
+    if (bn2.y.has_value() && bn2.y->defined()) {
+      check_bf16_nhwc(*bn2.y, "y2");
+      TORCH_CHECK(bn2.y->sizes() == y.sizes(), "y2 must have the shape of y");
+      TORCH_CHECK(bn2.stats.has_value() && bn2.stats->defined() && bn2.stats->numel() == 4 * s.C &&
+                  bn2.stats->scalar_type() == at::kFloat && bn2.stats->is_contiguous(), "stats2 must be fp32 [4, C]");
+      TORCH_CHECK(bn2.acc.has_value() && bn2.acc->defined() && bn2.acc->numel() == 2 * s.C &&
+                  bn2.acc->scalar_type() == at::kFloat && bn2.acc->is_contiguous() && bn2.acc->is_cuda(),
+                  "acc2 must be a contiguous fp32 [2, C] device tensor");
+      TORCH_CHECK(mask == 3 && ap != nullptr, "the second BN needs mask 3 and the residual addend");
+      bn.y2 = cbf(*bn2.y);
+      bn.stats2 = bn2.stats->data_ptr<float>();
+      bn.acc2 = bn2.acc->data_ptr<float>();
+    }
     launch(s, bf(dx), ap, &bn, st, asub);
     return {dx, acc->view({2, s.C})};
   }
@@ -262,6 +281,7 @@ std::tuple<Tensor, Tensor> dgrad_bn_core(const Tensor& dy_like, const pdt::ConvS
   auto sums = fbuf.narrow(0, 0, n_sums).view({2, s.C});
   auto part = fbuf.narrow(0, n_sums, n_part);
   auto ws = fbuf.narrow(0, n_sums + n_part, n_ws);
+  TORCH_CHECK(!(bn2.y.has_value() && bn2.y->defined()), "the second BN needs acc mode");
   pdt::BnBwdFuse bn{cbf(y), zp, stats.data_ptr<float>(), part.data_ptr<float>(), (int)mask};
   launch(s, bf(dx), ap, &bn, st, asub);
   float* dg = nullptr;
@@ -284,7 +304,9 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
                                          const std::optional<Tensor>& z, const Tensor& stats,
                                          int64_t mask, const std::optional<Tensor>& dgamma,
                                          const std::optional<Tensor>& dbeta,
-                                         const std::optional<Tensor>& wt_in, const std::optional<Tensor>& acc) {
+                                         const std::optional<Tensor>& wt_in, const std::optional<Tensor>& acc,
+                                         const std::optional<Tensor>& y2, const std::optional<Tensor>& stats2,
+                                         const std::optional<Tensor>& acc2) {
   check_bf16_nhwc(dy, "dy");
   TORCH_CHECK(xs.size() == 4, "x shape must be NHWC");
   TORCH_CHECK(xs[3] == w.size(1), "dgrad: x channels must equal weight in-channels");
@@ -292,7 +314,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& w, std:
   auto s = shape_of(xs[0], xs[1], xs[2], xs[3], w.size(0), w.size(2), w.size(3), stride, pad);
   TORCH_CHECK(s.Ho == dy.size(1) && s.Wo == dy.size(2) && s.K == dy.size(3), "dgrad: dy shape mismatch");
   Tensor wt = packed_t_or_pack(w, wt_in);
-  return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta, acc,
+  return dgrad_bn_core(dy, s, addend, y, z, stats, mask, dgamma, dbeta, acc, SecondBn{y2, stats2, acc2},
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad(cbf(dy), cbf(wt), dx, ap, sh, st, bn, asub);
@@ -390,7 +412,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fold(const Tensor& g, const Tensor& z_i
   pdt::DgradFold fold{cbf(z_in), C, bias.data_ptr<float>()};
   // acc: fp32-atomic BN sums of the unit before (default runs); without it (deterministic runs) the
   // fixed-order partials + reduce path, with that unit's dgamma / dbeta sinks
-  return dgrad_bn_core(g, s, std::nullopt, y, z, stats, mask, dgamma, dbeta, acc,
+  return dgrad_bn_core(g, s, std::nullopt, y, z, stats, mask, dgamma, dbeta, acc, SecondBn{},
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad(cbf(g), reinterpret_cast<const uint16_t*>(wfold.data_ptr()), dx,
@@ -444,7 +466,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn_fp8(const Tensor& dy8, const Tensor& wt
                                              const std::optional<Tensor>& acc) {
   c10::hip::HIPGuard g(dy8.get_device());
   auto s = fp8_dgrad_shape(dy8, wt8, wscale, ascale, xs, stride, pad);
-  return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta, acc,
+  return dgrad_bn_core(dy8, s, addend, y, z, stats, mask, dgamma, dbeta, acc, SecondBn{},
                        [&](const pdt::ConvShape& sh, uint16_t* dx, const uint16_t* ap, const pdt::BnBwdFuse* bn,
                            hipStream_t st, int asub) {
                          pdt::launch_conv_dgrad_fp8(dy8.data_ptr<uint8_t>(), wt8.data_ptr<uint8_t>(),
@@ -1456,7 +1478,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_dgrad_bn", checked("conv_dgrad_bn", &conv_dgrad_bn), py::arg("dy"), py::arg("w"),
         py::arg("x_shape"), py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("y"),
         py::arg("z"), py::arg("stats"), py::arg("mask"), py::arg("dgamma") = py::none(),
-        py::arg("dbeta") = py::none(), py::arg("wt") = py::none(), py::arg("acc") = py::none());
+        py::arg("dbeta") = py::none(), py::arg("wt") = py::none(), py::arg("acc") = py::none(),
+        py::arg("y2") = py::none(), py::arg("stats2") = py::none(), py::arg("acc2") = py::none());
   m.def("conv_wgrad", checked("conv_wgrad", &conv_wgrad), py::arg("dy"), py::arg("x"), py::arg("w_shape"), py::arg("stride"),
         py::arg("pad"), py::arg("deterministic") = false, py::arg("out") = py::none());
   m.def("conv_wgrad_side", checked("conv_wgrad_side", &conv_wgrad_side), py::arg("side"), py::arg("dy"),

@@ -100,6 +100,13 @@ struct NtArgs {
                           // ReLU bitmask: one byte per 8-channel chunk, bit q = (z[c0 + q] > 0)
   const float* bn_stats;  // [4][Nout] mean, invstd, scale, shift
   float* bn_part;
+  // second BatchNorm on the SAME gradient g (acc mode, mask 3 + addend only): a downsampling block's
+  // projection-shortcut BN, whose input gradient is that block's output gradient too.  Its y and
+  // mean, and an fp32 [2][Nout] accumulator of (sum g, sum g*(y2 - mean2)) -- the reduction pass the
+  // shortcut's BN backward would otherwise run over g and y2
+  const uint16_t* bn_y2;
+  const float* bn_stats2;
+  float* bn_acc2;
   float* bn_acc;  // non-null: fp32-atomic accumulation of the partials into [2][Nout] instead
   int bn_mask, bn_group0;
   // addend layout: 0 = same NHWC layout as out; 2 = compact stride-2 map addend[n][h/2][w/2] that
@@ -358,6 +365,8 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   static_assert(64 % CH_PER_ROW == 0, "a lane keeps one channel chunk across the store loop");
   // EPI_BNB: this lane's 8 channels are fixed (c = lane % CH_PER_ROW); per-lane partial sums
   float bmu[8], bsc[8], bsh[8], bsg[8], bsq[8];
+  float bmu2[8], bsq2[8];   // EPI_BNB with bn_y2: the second BN's mean and sum g*y2
+  const bool has_y2 = EPI == EPI_BNB && P.bn_y2 != nullptr;
   pdt_f2 st_s[4], st_q[4];  // EPI_STATS (store-loop form): the lane's 8 channels, as pairs
 #pragma unroll
   for (int h = 0; h < 4; ++h) { st_s[h] = pdt_f2{0.f, 0.f}; st_q[h] = pdt_f2{0.f, 0.f}; }
@@ -370,6 +379,8 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
       bsh[q] = P.bn_stats[3 * P.Nout + colb + q];
       bsg[q] = 0.f;
       bsq[q] = 0.f;
+      bsq2[q] = 0.f;
+      bmu2[q] = has_y2 ? P.bn_stats2[colb + q] : 0.f;
     }
   }
   // Two phases per batch of up to 8 chunks: first issue every global read the epilogue needs
@@ -392,10 +403,11 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   // Mask mode 3 (bitmask) masks the PACKED bf16 chunk: per pair of channels two sign-extended
   // bit fields merged by one v_bfi_b32 give the 32-bit keep-mask, so g is never unpacked, masked
   // and re-packed (the chunk was rounded to bf16 already: same bits as masking in fp32).
-  auto run_batches = [&](auto mm_c, auto ha_c, auto dn_c) {
+  auto run_batches = [&](auto mm_c, auto ha_c, auto dn_c, auto y2_c) {
     constexpr int MM = decltype(mm_c)::value;   // 0 none, 1 z > 0, 2 y*sc+sh > 0, 3 bitmask
     constexpr bool HA = decltype(ha_c)::value;  // residual-gradient addend
     constexpr bool DN = decltype(dn_c)::value;  // dense addressing fast path
+    constexpr bool Y2 = decltype(y2_c)::value;  // second BN's y (bn_y2)
     constexpr int RSTEP = 64 / CH_PER_ROW;      // staging rows advanced per chunk slot
     const int c_l = lane % CH_PER_ROW, r_l = lane / CH_PER_ROW;
     const int col_l = wcol0 + c_l * 8;
@@ -448,7 +460,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
           }
         }
       }
-      v4i av[IT], yv[IT], zv[IT];
+      v4i av[IT], yv[IT], zv[IT], y2v[Y2 ? IT : 1];
       if constexpr (HA) {
         const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.addend, P.add_bytes);
 #pragma unroll
@@ -458,6 +470,11 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
         const __amdgpu_buffer_rsrc_t rr = make_rsrc(P.bn_y, P.o_bytes);
 #pragma unroll
         for (int it = 0; it < IT; ++it) yv[it] = buf_load16(rr, ooff[it]);
+        if constexpr (Y2) {
+          const __amdgpu_buffer_rsrc_t r2 = make_rsrc(P.bn_y2, P.o_bytes);
+#pragma unroll
+          for (int it = 0; it < IT; ++it) y2v[it] = buf_load16(r2, ooff[it]);
+        }
         if constexpr (MM == 1) {
           const __amdgpu_buffer_rsrc_t rz = make_rsrc(P.bn_z, P.o_bytes);
 #pragma unroll
@@ -514,6 +531,11 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
             bsg[q] += a.v[q];
             bsq[q] = fmaf(a.v[q], yy.v[q], bsq[q]);  // sum g*y; the mean term comes off once below
           }
+          if constexpr (Y2) {
+            const f8 y2 = unpack8(__builtin_bit_cast(uint4, y2v[it]));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bsq2[q] = fmaf(a.v[q], y2.v[q], bsq2[q]);
+          }
         }
         if constexpr (EPI == EPI_STATS) {
           // rows past the GEMM edge were staged as 0 (their accumulators are 0): no mask needed
@@ -538,14 +560,23 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
   const bool has_add = P.addend != nullptr;
   const bool dense = P.dense && !(has_add && P.add_sub);
   auto with_dn = [&](auto mm, auto ha) {
-    if (dense) run_batches(mm, ha, HT{});
-    else run_batches(mm, ha, HF{});
+    if (dense) run_batches(mm, ha, HT{}, HF{});
+    else run_batches(mm, ha, HF{}, HF{});
   };
   if constexpr (EPI == EPI_BNB) {
     switch (P.bn_mask) {
       case 1: if (has_add) with_dn(M1{}, HT{}); else with_dn(M1{}, HF{}); break;
       case 2: if (has_add) with_dn(M2{}, HT{}); else with_dn(M2{}, HF{}); break;
-      case 3: if (has_add) with_dn(M3{}, HT{}); else with_dn(M3{}, HF{}); break;
+      case 3:
+        if (has_add && has_y2) {  // the hand-off dgrad of a downsampling block's output
+          if (dense) run_batches(M3{}, HT{}, HT{}, HT{});
+          else run_batches(M3{}, HT{}, HF{}, HT{});
+        } else if (has_add) {
+          with_dn(M3{}, HT{});
+        } else {
+          with_dn(M3{}, HF{});
+        }
+        break;
       default: if (has_add) with_dn(M0{}, HT{}); else with_dn(M0{}, HF{}); break;
     }
   } else {
@@ -615,7 +646,10 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
     // sum g*(y - mean) = sum g*y - mean * sum g per lane: one VALU per element less in the batch
     // loop above (the epilogue, not the MFMAs, bounds the short-K dgrads' issue)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bsq[q] = fmaf(-bmu[q], bsg[q], bsq[q]);
+    for (int q = 0; q < 8; ++q) {
+      bsq[q] = fmaf(-bmu[q], bsg[q], bsq[q]);
+      bsq2[q] = fmaf(-bmu2[q], bsg[q], bsq2[q]);
+    }
     // combine the lanes holding the same channel chunk (lane, lane+CH_PER_ROW, ...), then the
     // first CH_PER_ROW lanes write this wave's (rows group, channels) partials
 #pragma unroll
@@ -625,24 +659,38 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& P, v4f (&acc)[TM][TN],
         bsg[q] += __shfl_xor(bsg[q], o, 64);
         bsq[q] += __shfl_xor(bsq[q], o, 64);
       }
+    if (has_y2)
+#pragma unroll
+      for (int o = CH_PER_ROW; o < 64; o <<= 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bsq2[q] += __shfl_xor(bsq2[q], o, 64);
     // then the WM wave rows of the workgroup are summed in LDS (fixed order): one partial per
     // (workgroup row tile, channel).  Waves past the GEMM edge hold zeros.
     __syncthreads();  // every wave has finished reading its staging rows (red[] aliases them)
-    float* red = reinterpret_cast<float*>(smem);  // [WM][2][BN]
+    float* red = reinterpret_cast<float*>(smem);  // [WM][3][BN]
     if (lane < CH_PER_ROW) {
-      float* rp = red + (wm * 2) * BN + wn * TN * 16 + lane * 8;
+      float* rp = red + (wm * 3) * BN + wn * TN * 16 + lane * 8;
       *reinterpret_cast<float4*>(rp) = make_float4(bsg[0], bsg[1], bsg[2], bsg[3]);
       *reinterpret_cast<float4*>(rp + 4) = make_float4(bsg[4], bsg[5], bsg[6], bsg[7]);
       *reinterpret_cast<float4*>(rp + BN) = make_float4(bsq[0], bsq[1], bsq[2], bsq[3]);
       *reinterpret_cast<float4*>(rp + BN + 4) = make_float4(bsq[4], bsq[5], bsq[6], bsq[7]);
+      if (has_y2) {
+        *reinterpret_cast<float4*>(rp + 2 * BN) = make_float4(bsq2[0], bsq2[1], bsq2[2], bsq2[3]);
+        *reinterpret_cast<float4*>(rp + 2 * BN + 4) = make_float4(bsq2[4], bsq2[5], bsq2[6], bsq2[7]);
+      }
     }
     __syncthreads();
     if (t < BN && n0 + t < P.Nout) {
-      float S = 0.f, Q = 0.f;
+      float S = 0.f, Q = 0.f, Q2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
-        S += red[(w * 2) * BN + t];
-        Q += red[(w * 2 + 1) * BN + t];
+        S += red[(w * 3) * BN + t];
+        Q += red[(w * 3 + 1) * BN + t];
+        if (has_y2) Q2 += red[(w * 3 + 2) * BN + t];
+      }
+      if (has_y2) {  // the second BN's accumulator: same sum g, its own centred sum
+        unsafeAtomicAdd(P.bn_acc2 + n0 + t, S);
+        unsafeAtomicAdd(P.bn_acc2 + P.Nout + n0 + t, Q2);
       }
       if (P.bn_acc != nullptr) {  // the BN-backward apply reads the finished sums: no reduce launch
         unsafeAtomicAdd(P.bn_acc + n0 + t, S);
@@ -1833,6 +1881,12 @@ static void conv_dgrad_impl(const void* dy, const void* wt, const float* oscale,
       }
       if (bn != nullptr) {
         a.bn_y = bn->y; a.bn_z = bn->z; a.bn_stats = bn->stats; a.bn_part = bn->part; a.bn_acc = bn->acc;
+        if (bn->y2 != nullptr) {
+          if (bn->acc == nullptr || bn->acc2 == nullptr || bn->stats2 == nullptr || bn->mask != 3 || addend == nullptr)
+            throw std::runtime_error("conv_dgrad: the second BN (y2) needs acc mode, its accumulator and "
+                                     "statistics, mask 3 and the residual addend");
+          a.bn_y2 = bn->y2; a.bn_stats2 = bn->stats2; a.bn_acc2 = bn->acc2;
+        }
         a.bn_mask = bn->mask; a.bn_group0 = group0;
         group0 += ceil_div(a.M, conv_nt_group_rows(a.M, a.Nout, a.Kg * EB));
         if constexpr (OP != OP_BF16) {

@@ -106,6 +106,11 @@ struct BnBwdFuse {
   float* part;           // [G][2][C]
   int mask;
   float* acc = nullptr;  // non-null: partials fp32-atomically summed into [2][C] (part unused)
+  // optional second BN fed by the same g (a downsampling block's projection-shortcut BN): its y,
+  // statistics and [2][C] accumulator of (sum g, sum g*(y2 - mean2)); acc mode, mask 3, addend only
+  const uint16_t* y2 = nullptr;
+  const float* stats2 = nullptr;
+  float* acc2 = nullptr;
 };
 int conv_dgrad_bn_groups(const ConvShape& s, int elem_bytes = 2);
 // addend_sub = 2: addend is a compact [N, ceil(H/2), ceil(W/2), C] map added at even (h, w) only

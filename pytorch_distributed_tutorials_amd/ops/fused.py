@@ -90,6 +90,10 @@ def _lead_mark(tag: str) -> None:
 
 
 _COMPACT_ADDEND = True  # stride-2 shortcut dgrad compact
+# the projection-shortcut BN's backward sums taken in the next block's hand-off dgrad epilogue (the
+# same output gradient g feeds both BNs of a downsampling block): no reduction pass over g and y_ds
+_DUAL_BN = os.environ.get("PDT_DUAL_BN", "1") == "1"  # (A/B knob)
+DUAL_CALLS = 0  # shortcut BNs whose backward sums came from the hand-off epilogue (tests)
 
 
 def set_fp8(on: bool) -> None:
@@ -859,10 +863,13 @@ class _BnHandoff:
     dgrad epilogue.  The consumer deposits (g, sums); the producer uses them only if the
     gradient it receives IS that g (same storage: no other consumer added to it)."""
 
-    __slots__ = ("y", "stats", "gamma", "beta", "zmask", "deposit")
+    __slots__ = ("y", "stats", "gamma", "beta", "zmask", "deposit", "ds")
 
-    def __init__(self, y, stats, gamma, beta, zmask=None):
+    def __init__(self, y, stats, gamma, beta, zmask=None, ds=None):
         self.y, self.stats, self.gamma, self.beta, self.zmask = y, stats, gamma, beta, zmask
+        # ds: (y, stats, gamma) of the block's projection-shortcut BN -- fed by the same output
+        # gradient g, so the consumer's epilogue reduces it too (kernels.h BnBwdFuse::y2)
+        self.ds = ds
         self.deposit = None
 
 
@@ -971,7 +978,8 @@ class _ResidualBlock(torch.autograd.Function):
         ctx.in8 = ins8 if ctx.fp8b and _FP8_WGRAD else None  # fp8 weight-gradient operands
         _, y_last, st_last = outs[-1]
         ctx.handoff_out = _BnHandoff(y_last, st_last, tensors[5 * (nch - 1) + 1],
-                                     tensors[5 * (nch - 1) + 2], zmask)
+                                     tensors[5 * (nch - 1) + 2], zmask,
+                                     (y_ds, st_ds, tensors[5 * nch + 1]) if ds_cfg is not None and _DUAL_BN else None)
         return h
 
     @staticmethod
@@ -1083,11 +1091,16 @@ class _ResidualBlock(torch.autograd.Function):
                 return C.conv_dgrad_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_)
             return C.conv_dgrad(dy_, w_, xshape, st_, pd_, addend_, _packed_crsk(w_))
 
-        def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None, acc=None):
+        def dgrad_bn_any(dy_, d8_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg=None, sb=None, acc=None,
+                         bn2=None):
             if d8_ is not None and _fp8_dgrad_ok(d8_[0].shape[3], st_):
+                assert bn2 is None
                 wt8, wsc = _packed_crsk8(C, w_)
                 return C.conv_dgrad_bn_fp8(d8_[0], wt8, wsc, d8_[1], xshape, st_, pd_, addend_, y_, z_,
                                            stt_, mask_, sg, sb, acc)
+            if bn2 is not None:
+                return C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb,
+                                       _packed_crsk(w_), acc, bn2[0], bn2[1], bn2[2])
             return C.conv_dgrad_bn(dy_, w_, xshape, st_, pd_, addend_, y_, z_, stt_, mask_, sg, sb,
                                    _packed_crsk(w_), acc)
 
@@ -1113,7 +1126,16 @@ class _ResidualBlock(torch.autograd.Function):
             gradient that the first conv's dgrad epilogue adds (None when x needs none)"""
             st2, pd2, tr2, _, _ = ds_cfg
             wds = tensors[5 * nch]
-            sums_ds = bnreduce(5 * nch, g_short_, g_short_, y_ds, st_ds, 0)
+            if sums_ds_dep is not None:
+                # reduced by the next block's hand-off epilogue: the apply adds dgamma / dbeta and the
+                # weight gradient re-zeroes the accumulator (as for every acc-mode BN)
+                global DUAL_CALLS
+                DUAL_CALLS += 1
+                sums_ds = sums_ds_dep
+                deferred[5 * nch] = (sums_ds, _grad_sink(params[5 * nch + 1]), _grad_sink(params[5 * nch + 2]))
+                sunk.extend([params[5 * nch + 1], params[5 * nch + 2]])
+            else:
+                sums_ds = bnreduce(5 * nch, g_short_, g_short_, y_ds, st_ds, 0)
             dy_ds, _, d8_ds = apply(5 * nch, g_short_, g_short_, y_ds, st_ds, sums_ds, 0, tr2, False,
                                     ctx.needs_input_grad[0], in8[0] if in8 else None, st2)
             wgrad(5 * nch, dy_ds, x, st2, pd2, d8_ds, in8[0] if in8 else None)
@@ -1134,9 +1156,15 @@ class _ResidualBlock(torch.autograd.Function):
         # gradient arriving pre-masked and pre-reduced from the next block's dgrad epilogue?
         pre = None
         ho = ctx.handoff_out
+        sums_ds_dep = None  # the shortcut BN's (sum g, sum g*(y_ds - mean)) from the same epilogue
         if ho.deposit is not None:
-            g_dep, sums_dep, acc_dep = ho.deposit
+            g_dep, sums_dep, acc_dep, acc2_dep = ho.deposit
             ho.deposit = None
+            if acc2_dep is not None:
+                if g_dep.data_ptr() == dz.data_ptr() and g_dep.shape == dz.shape:
+                    sums_ds_dep = acc2_dep
+                else:
+                    acc2_dep.zero_()
             jl = 5 * (nch - 1)
             if g_dep.data_ptr() == dz.data_ptr() and g_dep.shape == dz.shape:
                 pre = (dz, sums_dep)
@@ -1249,13 +1277,19 @@ class _ResidualBlock(torch.autograd.Function):
                         zsrc, zmode = (hi.zmask, 3) if hi.zmask is not None else (x, 1)
                         if _BN_ACC and not det:
                             acc = _bacc(hi.gamma, hi.stats.shape[1])
+                            # the previous block's projection-shortcut BN reduced in the same epilogue
+                            ds2 = hi.ds if (hi.ds is not None and zmode == 3 and addend is not None
+                                            and (d8 is None or not _fp8_dgrad_ok(d8[0].shape[3], st))
+                                            and _grad_sink(hi.ds[2]) is not None) else None
+                            acc2 = _bacc(hi.ds[2], hi.stats.shape[1]) if ds2 is not None else None
                             dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
-                                                       hi.stats, zmode, acc=acc)
-                            hi.deposit = (dz, sums_in, acc)
+                                                       hi.stats, zmode, acc=acc,
+                                                       bn2=(ds2[0], ds2[1], acc2) if ds2 is not None else None)
+                            hi.deposit = (dz, sums_in, acc, acc2)
                         else:
                             dz, sums_in = dgrad_bn_any(dy, d8, w, list(x.shape), st, pd, addend, hi.y, zsrc,
                                                        hi.stats, zmode, sg, sb)
-                            hi.deposit = (dz, sums_in, None)
+                            hi.deposit = (dz, sums_in, None, None)
                     else:
                         dz = dgrad(dy, d8, w, list(x.shape), st, pd, addend)
         ctx.handoff_in = None

@@ -103,7 +103,7 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc
 
     ddp.space.grad_flat.zero_()
     ddp.space.attach_grads()
-    folds0 = fused.FOLD_CALLS
+    folds0, duals0 = fused.FOLD_CALLS, fused.DUAL_CALLS
     out_n = blocks_n[1].forward_native(blocks_n[0].forward_native(x_n))
     out_r = blocks_r[1](blocks_r[0](x_r))
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -116,6 +116,10 @@ def test_block_pair_train_mode_vs_fp32(models, gpu, arch, stage, cin, hw, bn_acc
     # the folded BN backward (ops.fused DgradFold) runs in block 0's last unit of a Bottleneck pair
     # whenever the atomic BN sums are on
     assert (fused.FOLD_CALLS > folds0) == (bool(bn_acc) and arch == "resnet50"), (fused.FOLD_CALLS, folds0)
+    # block 0 of every stage pair with a projection shortcut takes that BN's backward sums from block
+    # 1's hand-off epilogue (atomic BN sums only)
+    has_ds = blocks_n[0].downsample is not None
+    assert (fused.DUAL_CALLS > duals0) == (bn_acc is True and has_ds), (fused.DUAL_CALLS, duals0)
 
     errs, yard = {}, {}
     errs["out"] = _rel(out_n.permute(0, 3, 1, 2), out_r)
