@@ -335,7 +335,7 @@ std::tuple<Tensor, Tensor> bn_fold_weights(const Tensor& wt, const Tensor& stats
   TORCH_CHECK(sums.scalar_type() == at::kFloat && sums.is_contiguous() && sums.numel() == 2 * K, "sums: fp32 [2, K]");
   c10::hip::HIPGuard g(wt.get_device());
   auto wfold = at::empty({C, K + C}, wt.options());
-  auto bias_ws = at::empty({C + 2 * K}, stats.options());  // bias, then the kernel's coefficient scratch
+  auto bias_ws = at::empty({pdt::bn_fold_weights_ws_floats(C, K)}, stats.options());  // bias, then the kernel's scratch
   auto bias = bias_ws.narrow(0, 0, C);
   pdt::launch_bn_fold_weights(reinterpret_cast<const uint16_t*>(wt.data_ptr()), stats.data_ptr<float>(),
                               gamma.data_ptr<float>(), sums.data_ptr<float>(), (int)count, C, K,

@@ -326,7 +326,8 @@ __global__ void __launch_bounds__(256) bn_fold_coef_kernel(FoldCoef cf, float* _
 __global__ void __launch_bounds__(256) bn_fold_weights_kernel(const uint16_t* __restrict__ wt, FoldCoef cf,
                                                               const float* __restrict__ coef, int C, int nG,
                                                               uint16_t* __restrict__ wfold,
-                                                              float* __restrict__ bias) {
+                                                              float* __restrict__ bias,
+                                                              float* __restrict__ part) {
   // on the critical stream, sharing SIMDs with the side stream's weight-gradient waves: ask for
   // issue priority over them
   __builtin_amdgcn_s_setprio(3);
@@ -346,8 +347,6 @@ __global__ void __launch_bounds__(256) bn_fold_weights_kernel(const uint16_t* __
     *reinterpret_cast<uint4*>(wfold + (size_t)c * KC + k) = pack8(v);
     return;
   }
-  __shared__ float red[3][16][64];
-  __shared__ float bred[3][64];
   const int nt = C / 32;
   const int ti = bid / nt, tj = bid - ti * nt;
   const int c0 = ti * 32, d0 = tj * 32;
@@ -400,21 +399,28 @@ __global__ void __launch_bounds__(256) bn_fold_weights_kernel(const uint16_t* __
       for (int q = 0; q < B4; ++q) { xa[q] = ya[q]; xb[q] = yb[q]; }
     }
   }
+  // the K-quarter partials meet in this block's slice of the global scratch `part`, not in LDS: a
+  // kernel that declares LDS waits for a CU with that much LDS free, and the side stream's
+  // weight-gradient blocks hold 128-160 KB of a CU's 160 KB for their whole K range (the 13-KB-LDS
+  // version ran 74-83 us per call in layer 1 against ~10 us of work, r9e).  __syncthreads orders
+  // the global stores and loads at workgroup scope.
+  float* pw = part + (size_t)bid * (3 * 17 * 64);
   if (wv > 0) {
+    float* q = pw + (wv - 1) * (17 * 64);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) red[wv - 1][e][lane] = acc[e];
-    bred[wv - 1][lane] = bacc;
+    for (int e = 0; e < 16; ++e) q[e * 64 + lane] = acc[e];
+    q[16 * 64 + lane] = bacc;
   }
   __syncthreads();
   if (wv != 0) return;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const float v = acc[e] + red[0][e][lane] + red[1][e][lane] + red[2][e][lane];
+    const float v = acc[e] + pw[e * 64 + lane] + pw[17 * 64 + e * 64 + lane] + pw[34 * 64 + e * 64 + lane];
     const int row = 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
     wfold[(size_t)(c0 + row) * KC + K + d0 + (lane & 31)] = f2bf(v);
   }
   if (with_bias) {
-    bacc += bred[0][lane] + bred[1][lane] + bred[2][lane];
+    bacc += pw[16 * 64 + lane] + pw[33 * 64 + lane] + pw[50 * 64 + lane];
     bacc += __shfl_xor(bacc, 32, 64);  // the two k halves of row r
     if (lane < 32) bias[c0 + r] = bacc;
   }
@@ -563,6 +569,8 @@ void launch_bn_fold_wgrad(float* t1, float* gram, const float* colsum, const uin
                      colsum, wt, cf, C, out, dgamma, dbeta, done, zero_sums ? 1 : 0, csum_slots);
 }
 
+int64_t bn_fold_weights_ws_floats(int C, int K) { return C + 2 * (int64_t)K + (int64_t)(C / 32) * (C / 32) * 3 * 17 * 64; }
+
 void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
                             int M, int C, int K, uint16_t* wfold, float* bias, hipStream_t st) {
   if (C % 32 != 0 || K % 256 != 0 || K > kFoldMaxK)
@@ -570,9 +578,13 @@ void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float*
   const int nG = (C / 32) * (C / 32);
   const int nS = (int)(((int64_t)C * K / 8 + 255) / 256);
   FoldCoef cf{stats, gamma, sums, K, 1.f / (float)M};
-  float* coef = bias + C;  // [2][K] scratch after the bias (the caller allocates C + 2K floats)
+  // scratch after the bias (the caller allocates bn_fold_weights_ws_floats(C, K)): coef [2][K],
+  // then the G tiles' cross-wave partials [nG][3][17][64]
+  float* coef = bias + C;
+  float* part = coef + 2 * K;
   hipLaunchKernelGGL(bn_fold_coef_kernel, dim3(ceil_div(K, 256)), dim3(256), 0, st, cf, coef);
-  hipLaunchKernelGGL(bn_fold_weights_kernel, dim3(nG + nS), dim3(256), 0, st, wt, cf, coef, C, nG, wfold, bias);
+  hipLaunchKernelGGL(bn_fold_weights_kernel, dim3(nG + nS), dim3(256), 0, st, wt, cf, coef, C, nG, wfold, bias,
+                     part);
 }
 
 __global__ void bn_eval_params_kernel(const float* rm, const float* rv, const float* gamma,

@@ -129,6 +129,7 @@ struct DgradFold {
 // 1x1 conv with transposed bf16
 // weights wt[C][K], BN statistics stats[4][K] (mean, invstd, ...), gamma[K] and backward sums
 // sums[2][K] (sum g, sum g*(y - mean)) over M rows
+int64_t bn_fold_weights_ws_floats(int C, int K);  // bias + coefficient / partials scratch
 void launch_bn_fold_weights(const uint16_t* wt, const float* stats, const float* gamma, const float* sums,
                             int M, int C, int K, uint16_t* wfold, float* bias, hipStream_t st);
 // its weight gradient: out[K][C] += diag(k1) t1 + diag(a) W gram + b colsum^T (t1 = g^T x [K][C],

@@ -13,6 +13,7 @@ bucket order.  Consequences:
 from __future__ import annotations
 
 import operator
+import os
 import weakref
 from typing import Dict, List, Optional, Sequence
 
@@ -27,6 +28,9 @@ def _is_dense(t: torch.Tensor) -> bool:
 
 
 _VERSION = operator.attrgetter("_version")
+# the dgrad-layout pack after each optimizer step on the weight-gradient stream (beside the next
+# forward) or on the caller's stream (PDT_PACK_SIDE=0)
+_PACK_SIDE = os.environ.get("PDT_PACK_SIDE", "1") == "1"
 # mirrors with a side-stream pack whose event no stream has waited on yet
 _PENDING_PACKS: "weakref.WeakSet" = weakref.WeakSet()
 
@@ -319,7 +323,7 @@ class WeightMirror:
     def after_optimizer_step(self) -> None:
         """The fused SGD step just wrote ``krsc``; rebuild ``crsk`` and mark both current."""
         self.space.version += 1
-        self._pack_t(side=True)
+        self._pack_t(side=_PACK_SIDE)
         self.key = self.current_key()
         self._trusted = None
 
