@@ -1592,6 +1592,8 @@ PYBIND11_MODULE(_C, m) {
     const int got = pdt::nt_timing_fetch(reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), n);
     return out.narrow(0, 0, got);
   }, py::arg("n"));
+  m.def("xgmi_force_chunks", &pdt::xgmi_force_chunks, py::arg("n") = -1,
+        "test hook: RS -> AG chunks per xGMI bucket (1..4), -1 = the size policy");
   m.def("conv_nt_force", &pdt::conv_nt_force, py::arg("k32") = -1, py::arg("mid") = -1, py::arg("wide") = -1);
   m.def("conv_nt_tile", [](int M, int Nout, int kg_bytes) {
     int bm = 0, bn = 0;

@@ -31,7 +31,7 @@ XgmiComm::XgmiComm(int rank, int world, int device, int64_t numel, int nbuckets,
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   hipc(hipMalloc(&g_, numel * sizeof(float)), "hipMalloc(grad)");
   hipc(hipMalloc(&red_, numel * sizeof(float)), "hipMalloc(reduced)");
-  const size_t fbytes = (size_t)nbuckets * 2 * 8 * sizeof(unsigned);
+  const size_t fbytes = (size_t)nbuckets * xgmi_slots_per_bucket() * 8 * sizeof(unsigned);
   // The per-bucket epoch flags are stored into by PEER GPUs and spin-polled here: keep them in
   // uncached (fine-grained) device memory, as RCCL does for its cross-GPU flags and FIFOs, so a
   // poll never hits a stale line of the local L2 whatever the coherence of peer stores through

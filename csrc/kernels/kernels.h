@@ -341,6 +341,8 @@ struct XgmiBuffers {
   const uint16_t* red16[8];
 };
 int xgmi_max_ranks();
+int xgmi_slots_per_bucket();   // flag slots per bucket: ready + one reduced slot per chunk
+void xgmi_force_chunks(int n);  // test hook: chunks per bucket (1..4), -1 = size policy
 int64_t xgmi_shard(int64_t lo, int64_t count, int world);
 void launch_xgmi_bucket(const XgmiBuffers& bufs, int world, int rank, int bucket, int64_t lo, int64_t count,
                         unsigned epoch, bool average, uint64_t timeout_ticks, unsigned* err, hipStream_t st,

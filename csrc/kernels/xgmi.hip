@@ -47,6 +47,12 @@ namespace pdt {
 
 constexpr int kXgmiMaxRanks = 8;
 constexpr unsigned kXgmiPoison = 0xffffffffu;  // flag value: the signalling rank has failed
+// RS -> AG pipelining: a bucket's shards are reduced, published and gathered in up to
+// kXgmiMaxChunks chunks, so the all-gather of chunk c starts while peers still reduce chunk c+1
+// (one reduced-flag slot per chunk; the ready slot is shared)
+constexpr int kXgmiMaxChunks = 4;
+constexpr int kXgmiSlotsPerBucket = 1 + kXgmiMaxChunks;
+constexpr int64_t kXgmiMinChunk = 1 << 18;  // elements of one rank's shard per chunk (1 MB fp32)
 
 struct XgmiPtrs {
   const float* g[kXgmiMaxRanks];    // every rank's gradient buffer (own included)
@@ -272,10 +278,11 @@ __global__ void __launch_bounds__(256) xgmi_pack_bf16_kernel(XgmiPtrs P, int ran
 // g_own[i] = red_{q}[i] / world (average) or red_q[i] (sum) for i in shard q of the bucket
 // [lo, hi): shard q = [max(lo, base + q*shard), min(hi, base + (q+1)*shard)), base = lo rounded
 // down to 8.  A failed rank writes NaN over the bucket instead (poison; see the header).
+// Chunk [sub_off, sub_off + sub_len) of every shard (the whole shard: 0, shard).
 template <bool BF16>
 __global__ void __launch_bounds__(256) xgmi_all_gather_kernel(XgmiPtrs P, int world, int rank, int64_t lo,
-                                                              int64_t hi, int64_t shard, int average,
-                                                              const unsigned* err) {
+                                                              int64_t hi, int64_t shard, int64_t sub_off,
+                                                              int64_t sub_len, int average, const unsigned* err) {
   float* g = const_cast<float*>(P.g[rank]);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -289,7 +296,9 @@ __global__ void __launch_bounds__(256) xgmi_all_gather_kernel(XgmiPtrs P, int wo
   const float w = average ? (float)world : 1.0f;
   const int64_t base = lo / 8 * 8;
   for (int q = 0; q < world; ++q) {
-    const int64_t a = std::max(lo, std::min(hi, base + q * shard)), b = std::min(hi, base + (q + 1) * shard);
+    const int64_t s0 = base + q * shard;
+    const int64_t a = std::max(lo, std::min(hi, s0 + sub_off));
+    const int64_t b = std::min(hi, std::min(s0 + shard, s0 + sub_off + sub_len));
     if (a >= b) continue;
     if constexpr (BF16) {
       const uint16_t* r16 = P.red16[q];
@@ -343,6 +352,19 @@ static void check(const char* what) {
 }
 
 int xgmi_max_ranks() { return kXgmiMaxRanks; }
+int xgmi_slots_per_bucket() { return kXgmiSlotsPerBucket; }
+
+// Test hook: pin the chunk count of every bucket (1..kXgmiMaxChunks), or -1 for the size policy.
+static int g_xgmi_chunks = -1;
+void xgmi_force_chunks(int n) { g_xgmi_chunks = n; }
+
+// chunks per bucket: one per kXgmiMinChunk elements of a shard, at most kXgmiMaxChunks; world 1
+// has no peers to overlap with
+static int xgmi_chunks(int64_t shard, int world) {
+  if (g_xgmi_chunks > 0) return std::min(kXgmiMaxChunks, g_xgmi_chunks);
+  if (world <= 1) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kXgmiMaxChunks, shard / kXgmiMinChunk));
+}
 
 // shard of the bucket [lo, lo + count): a multiple of 8 elements counted from lo rounded down to
 // 8, so every interior shard boundary is 32-B aligned (float4 / 8 x bf16 units stay whole); the
@@ -371,7 +393,10 @@ void launch_xgmi_bucket(const XgmiBuffers& B, int world, int rank, int bucket, i
   const int64_t base = lo / 8 * 8;
   const int64_t own_lo = std::max(lo, std::min(hi, base + rank * shard));
   const int64_t own_hi = std::min(hi, base + (rank + 1) * shard);
-  const int slot_ready = bucket * 2, slot_red = bucket * 2 + 1;
+  const int slot_ready = bucket * kXgmiSlotsPerBucket;
+  const int nch = xgmi_chunks(shard, world);
+  const int64_t cs = ((shard + nch - 1) / nch + 7) / 8 * 8;  // chunk of a shard, 32-B aligned
+  auto slot_red = [&](int c) { return slot_ready + 1 + c; };
   const int cap = std::max(1, max_blocks);
   auto blocks = [&](int64_t units) {
     const int64_t b = (units + 255) / 256;
@@ -379,8 +404,10 @@ void launch_xgmi_bucket(const XgmiBuffers& B, int world, int rank, int bucket, i
   };
   auto on = [&](int ph) { return ph >= phase_lo && ph <= phase_hi; };
   // phase 0: (bf16 wire: pack) + signal ready, 1: wait ready, 2: reduce-scatter, 3: signal
-  // reduced, 4: wait reduced, 5: all-gather.  In-process rank groups enqueue phase-major so that
-  // no rank's wait can sit in a hardware queue ahead of another rank's signal.
+  // reduced, 4: wait reduced, 5: all-gather.  Chunked buckets run phase 2 as (reduce-scatter,
+  // signal) per chunk and phase 4 as (wait, all-gather) per chunk; phases 3 and 5 are then empty.
+  // In-process rank groups enqueue phase-major so that no rank's wait can sit in a hardware queue
+  // ahead of another rank's signal.
   if (on(0)) {
     if (bf16)
       hipLaunchKernelGGL(xgmi_pack_bf16_kernel, dim3(blocks(count / 8 + 1)), dim3(256), 0, st, P, rank, lo, hi);
@@ -392,29 +419,51 @@ void launch_xgmi_bucket(const XgmiBuffers& B, int world, int rank, int bucket, i
   // world 1, fp32 wire: the reduced bucket IS the gradient (sum of one rank, divided by 1) --
   // only the flag protocol runs (RCCL's world-1 all-reduce is likewise no data movement)
   const bool data = world > 1 || bf16;
-  if (on(2) && data && own_hi > own_lo) {
-    const unsigned grid = blocks((own_hi - own_lo) / (bf16 ? 8 : 4 * kXgmiUnroll) + 1);
+  const int64_t s_own = base + rank * shard;
+  auto rs = [&](int64_t a, int64_t b) {
+    if (!data || b <= a) return;
+    const unsigned grid = blocks((b - a) / (bf16 ? 8 : 4 * kXgmiUnroll) + 1);
     switch (world) {
-      case 1: launch_rs<1>(P, bf16, world, rank, own_lo, own_hi, grid, err, st); break;
-      case 2: launch_rs<2>(P, bf16, world, rank, own_lo, own_hi, grid, err, st); break;
-      case 4: launch_rs<4>(P, bf16, world, rank, own_lo, own_hi, grid, err, st); break;
-      case 8: launch_rs<8>(P, bf16, world, rank, own_lo, own_hi, grid, err, st); break;
-      default: launch_rs<0>(P, bf16, world, rank, own_lo, own_hi, grid, err, st); break;
+      case 1: launch_rs<1>(P, bf16, world, rank, a, b, grid, err, st); break;
+      case 2: launch_rs<2>(P, bf16, world, rank, a, b, grid, err, st); break;
+      case 4: launch_rs<4>(P, bf16, world, rank, a, b, grid, err, st); break;
+      case 8: launch_rs<8>(P, bf16, world, rank, a, b, grid, err, st); break;
+      default: launch_rs<0>(P, bf16, world, rank, a, b, grid, err, st); break;
     }
-  }
-  if (on(3))
-    hipLaunchKernelGGL(xgmi_signal_kernel, dim3(1), dim3(64), 0, st, P, world, rank, slot_red, epoch, err);
-  if (on(4))
-    hipLaunchKernelGGL(xgmi_wait_kernel, dim3(1), dim3(64), 0, st, P.flags[rank], world, slot_red, epoch,
-                       (unsigned long long)timeout_ticks, err, 2u + 2u * (unsigned)bucket);
-  if (on(5) && data) {
-    const unsigned grid = blocks(shard / (bf16 ? 8 : 4 * kXgmiUnroll) + 1);
+  };
+  auto ag = [&](int64_t sub_off, int64_t sub_len) {
+    if (!data) return;
+    const unsigned grid = blocks(sub_len / (bf16 ? 8 : 4 * kXgmiUnroll) + 1);
     if (bf16)
       hipLaunchKernelGGL(xgmi_all_gather_kernel<true>, dim3(grid), dim3(256), 0, st, P, world, rank, lo, hi, shard,
-                         average ? 1 : 0, err);
+                         sub_off, sub_len, average ? 1 : 0, err);
     else
       hipLaunchKernelGGL(xgmi_all_gather_kernel<false>, dim3(grid), dim3(256), 0, st, P, world, rank, lo, hi, shard,
-                         average ? 1 : 0, err);
+                         sub_off, sub_len, average ? 1 : 0, err);
+  };
+  auto wait_red = [&](int c) {
+    hipLaunchKernelGGL(xgmi_wait_kernel, dim3(1), dim3(64), 0, st, P.flags[rank], world, slot_red(c), epoch,
+                       (unsigned long long)timeout_ticks, err, 2u + 2u * (unsigned)bucket);
+  };
+  auto signal_red = [&](int c) {
+    hipLaunchKernelGGL(xgmi_signal_kernel, dim3(1), dim3(64), 0, st, P, world, rank, slot_red(c), epoch, err);
+  };
+  if (nch == 1) {
+    if (on(2)) rs(own_lo, own_hi);
+    if (on(3)) signal_red(0);
+    if (on(4)) wait_red(0);
+    if (on(5)) ag(0, shard);
+  } else {
+    if (on(2))
+      for (int c = 0; c < nch; ++c) {
+        rs(std::max(lo, std::min(hi, s_own + c * cs)), std::min(hi, std::min(s_own + shard, s_own + (c + 1) * cs)));
+        signal_red(c);
+      }
+    if (on(4))
+      for (int c = 0; c < nch; ++c) {
+        wait_red(c);
+        ag(c * cs, cs);
+      }
   }
   check("xgmi bucket");
 }

@@ -28,9 +28,11 @@ def _is_dense(t: torch.Tensor) -> bool:
 
 
 _VERSION = operator.attrgetter("_version")
-# the dgrad-layout pack after each optimizer step on the weight-gradient stream (beside the next
-# forward) or on the caller's stream (PDT_PACK_SIDE=0)
-_PACK_SIDE = os.environ.get("PDT_PACK_SIDE", "1") == "1"
+# the dgrad-layout pack after each optimizer step: on the caller's stream right behind the update
+# (default), or on the weight-gradient stream beside the next forward (PDT_PACK_SIDE=1).  Same call,
+# ResNet-50 b256, four runs each: 17.88 ms vs 17.91 (s25) -- the side-stream fork's marker and
+# cross-queue waits at the step boundary cost more than the 25 us pack.
+_PACK_SIDE = os.environ.get("PDT_PACK_SIDE", "0") == "1"
 # mirrors with a side-stream pack whose event no stream has waited on yet
 _PENDING_PACKS: "weakref.WeakSet" = weakref.WeakSet()
 

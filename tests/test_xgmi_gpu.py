@@ -27,8 +27,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("chunks", [-1, 3])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_xgmi_in_process_ranks_bitwise(gpu, world):
+def test_xgmi_in_process_ranks_bitwise(gpu, world, chunks, native_ext):
+    """chunks 3: every bucket reduced, published and gathered in three RS -> AG pipelined chunks
+    (xgmi.hip kXgmiMaxChunks; the size policy keeps these small buckets whole)"""
+    native_ext.xgmi_force_chunks(chunks)
+    try:
+        _in_process_ranks_bitwise(gpu, world)
+    finally:
+        native_ext.xgmi_force_chunks(-1)
+
+
+def _in_process_ranks_bitwise(gpu, world):
     from pytorch_distributed_tutorials_amd.parallel.xgmi import local_group, reduce_local_group
     n = 300_007
     buckets = [(0, 100_000), (100_000, 123_457), (223_457, 76_550)]
