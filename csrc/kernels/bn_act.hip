@@ -8,6 +8,7 @@
 // (dz, z, y) and one elementwise pass producing dy and the residual gradient.
 #include "common.h"
 #include "fp8_util.h"
+#include "igemm_common.h"
 #include "kernels.h"
 #include "pool_quad.h"
 
@@ -1210,7 +1211,9 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(const uint4* __res
                                                               uint2* __restrict__ idx,
                                                               uint4* __restrict__ uarg, uint32_t total,
                                                               int H, int W, int lc8, int Ho, int Wo) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD-contiguous block order: the output rows one XCD pools in turn share their input rows
+  // (stride 2, window 3) in that XCD's L2, instead of every row pair straddling two XCDs
+  const uint32_t t = (uint32_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int C8 = 1 << lc8;
   const int c8 = (int)(t & (uint32_t)(C8 - 1));

@@ -147,7 +147,33 @@ __global__ void __launch_bounds__(256) avgpool_bwd_kernel(const float* __restric
   }
 }
 
+// 8 channels per thread (16-byte loads; the scalar form's 2-byte loads ran the ResNet-50 head,
+// 256 x 7 x 7 x 2048, at ~1.4 TB/s: 18.5 us in-step).  Same fixed summation order per channel.
+__global__ void __launch_bounds__(256) avgpool_fwd8_kernel(const uint4* __restrict__ x, float4* __restrict__ y,
+                                                           int HW, int C8, int64_t total) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int64_t n = t / C8, c8 = t - n * C8;
+  const uint4* p = x + n * HW * C8 + c8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 7
+  for (int i = 0; i < HW; ++i) {
+    const f8 v = unpack8(p[(int64_t)i * C8]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += v.v[j];
+  }
+  const float inv = (float)HW;
+  y[2 * t] = make_float4(s[0] / inv, s[1] / inv, s[2] / inv, s[3] / inv);
+  y[2 * t + 1] = make_float4(s[4] / inv, s[5] / inv, s[6] / inv, s[7] / inv);
+}
+
 void launch_avgpool_fwd(const uint16_t* x, float* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+    const int64_t total = (int64_t)N * (C / 8);
+    hipLaunchKernelGGL(avgpool_fwd8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(x), reinterpret_cast<float4*>(y), HW, C / 8, total);
+    return;
+  }
   hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ceil_div(C, 256), N), dim3(256), 0, st, x, y, HW, C);
 }
 

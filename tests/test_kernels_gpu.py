@@ -281,6 +281,8 @@ def test_avgpool(gpu, native_ext):
     x = torch.randn(4, 7, 7, 2048, device=gpu).to(torch.bfloat16)
     y = C.avgpool_fwd(x)
     assert torch.allclose(y, x.float().mean((1, 2)), atol=1e-3)
+    x2 = torch.randn(3, 3, 5, 40, device=gpu).to(torch.bfloat16)  # odd spatial size, 5 vectors per pixel
+    assert torch.allclose(C.avgpool_fwd(x2), x2.float().mean((1, 2)), atol=1e-3)
     dy = torch.randn(4, 2048, device=gpu)
     dx = C.avgpool_bwd(dy, 7, 7)
     assert torch.allclose(dx.float(), (dy / 49)[:, None, None, :].expand(4, 7, 7, 2048), atol=1e-3, rtol=1e-2)
