@@ -235,7 +235,10 @@ def main(argv=None) -> int:
         holder["ddp"] = ddp
         if args.comm_timing:
             ddp.enable_comm_timing(True)
-        opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5)
+        # graph replay keeps the post-backward update: with the per-bucket update's local-mode
+        # reducer attached, the replayed ResNet-18/CIFAR step ran 5.3 ms instead of 1.98 (s36)
+        opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-5,
+                  overlap=False if args.graph else None)
         criterion = ops.CrossEntropyLoss()
         autocast = None
     else:

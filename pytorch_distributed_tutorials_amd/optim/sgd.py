@@ -25,6 +25,8 @@ backwards are not updated (their gradients accumulate as usual).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import reference as ref
@@ -45,6 +47,8 @@ class SGD(torch.optim.Optimizer):
         self._flat_first = {}   # flat space id -> the next update initialises the momentum buffer
         self._armed = None      # hyperparameters the reducer's per-bucket update was armed with
         self._overlap_owner = None
+        if overlap is None and os.environ.get("PDT_OPT_OVERLAP", "1") == "0":
+            overlap = False
         if overlap is not False:
             self._attach_overlap()
 

@@ -238,7 +238,10 @@ def main(argv: Optional[list] = None) -> int:
     if args.log_every:
         ddp_model.enable_comm_timing(True)
     inject = FaultInjector(env.rank)
-    optimizer = SGD(ddp_model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5)
+    # a captured step keeps the post-backward update (the per-bucket one's local-mode reducer made
+    # graph replay ~2.7x slower, bench.py --graph)
+    optimizer = SGD(ddp_model.parameters(), lr=args.learning_rate, momentum=0.9, weight_decay=1e-5,
+                    overlap=False if args.graph else None)
 
     model_filepath = os.path.join(args.model_dir, args.model_filename)
     start_epoch = 0
